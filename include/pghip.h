@@ -1,0 +1,94 @@
+/* libpghip — MI355X (gfx950) kernels for the PaliGemma image->text path.
+ *
+ * Drop-in boundary.  The reference has no FFI: its interface is the Python module API
+ * (SURVEY.md §8(b)).  The Python drop-in modules in paligemma-multimodal-system_amd/
+ * (modeling_siglip.py, modeling_gemma.py, modeling_paligemma.py, inference.py) keep
+ * that API and call ONLY these entry points (through ctypes, pghip/_lib.py).  Each
+ * entry point replaces the torch ops at the reference call sites cited below.
+ *
+ * Conventions: plain device pointers + sizes; every call enqueues on `stream`
+ * (hipStream_t; pass torch.cuda.current_stream().cuda_stream), never allocates,
+ * never synchronises, and returns 0 or a hipError_t code (hipErrorInvalidValue for
+ * a rejected shape).  bf16 = IEEE bfloat16 bits in uint16; "f32" = float.
+ * Buffers are owned by the caller (PyTorch's caching allocator).
+ */
+#ifndef PGHIP_H
+#define PGHIP_H
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int pg_abi_version(void);
+
+/* Epilogues of pg_gemm */
+enum {
+  PG_EPI_BF16 = 0,          /* C bf16 = acc + bias                                              */
+  PG_EPI_BF16_GELU = 1,     /* C bf16 = gelu_tanh(acc + bias)          SiglipMLP fc1 (siglip:183-184) */
+  PG_EPI_BF16_GELU_MUL = 2, /* C bf16 [M][N/2] = gelu(gate)*up, W rows interleaved 16 gate/16 up
+                               GemmaMLP gate/up (gemma:212-217)                                  */
+  PG_EPI_F32 = 3,           /* C f32 [ksplit][M][ldc] partial slabs (+bias on slab 0)          */
+  PG_EPI_F32_POS = 4,       /* C f32 = acc + bias + aux[(m % aux_rows)*ldc + n]   patch+pos emb  */
+  PG_EPI_BF16_VT = 5        /* cols < aux_n -> C bf16; cols >= aux_n -> aux_out[(n-aux_n)*aux_ld + m] */
+};
+
+/* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
+ * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0
+ * (% 64 when M > 16), N % 4 == 0.  M <= 16 takes the weight-streaming GEMV path. */
+int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
+            int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
+            int aux_ld, int aux_n, hipStream_t stream);
+
+/* resid[row] += sum_s partials[s][row]; y = LayerNorm (mode 0, w, b) | Gemma RMSNorm (mode 1, (1+w)).
+ * siglip.py:199,203,210,218,310,319 ; gemma.py:157-182,395,412,470.  y -> out bf16 (ldo) and/or out_f32. */
+int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part, const float* w,
+                     const float* b, void* out, int ldo, float* out_f32, const int* row_map, int M_out,
+                     int H, int mode, float eps, int write_resid, hipStream_t stream);
+
+/* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
+ * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
+ * split-KV partials, merge with pg_attn_combine. */
+int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
+                 long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
+                 long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
+                 int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
+                 hipStream_t stream);
+int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
+                    void* o, long o_rs, hipStream_t stream);
+
+/* RoPE (gemma.py:112-151) on q in place and k; k -> cache rows, v -> transposed cache (KVCache.update
+ * gemma.py:18-57 as a static in-place append). */
+int pg_rope_kv_write(void* qkv, int ldq, const int* pos, int T, int L, int Hq, int Hkv, int D,
+                     const float* cosT, const float* sinT, void* kc, void* vtc, int Smax, int slot_base,
+                     const int* slot_dev, hipStream_t stream);
+
+/* Conv2d(k=s=patch, valid) input rows (siglip.py:258-263,285). */
+int pg_patch_im2col(const float* px, int B, int C, int H, int W, int p, void* out, int ldk, hipStream_t stream);
+
+/* masked_scatter order of image tokens (paligemma.py:121-122): exclusive count. */
+int pg_image_rank(const int64_t* ids, int n, long image_id, int* rank, hipStream_t stream);
+
+/* embed gather + merge + pad zero + *sqrt(H)  (paligemma.py:99-128,288 ; gemma.py:510-511). */
+int pg_embed_merge(const int64_t* ids, const int* rank, int n, const void* embed, int V, const float* feat,
+                   int n_feat, int H, long image_id, long pad_id, float img_scale, float normalizer,
+                   float* out, hipStream_t stream);
+
+/* greedy next token (inference.py:59,68), first index on ties; optional decode-state advance. */
+int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
+              int64_t* hist, int* step, int* pos, int* kv_len, hipStream_t stream);
+
+/* softmax(logits/T) + top-p filter (inference.py:65,90-102) + explicit-uniform inverse-CDF draw. */
+int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature, float top_p,
+                   const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
+                   int* kv_len, float* probs_out, hipStream_t stream);
+
+/* name-seeded synthetic weights, bit-identical to oracle/synth.py (out_kind 0 bf16, 1 f32). */
+int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, int out_kind,
+                  hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGHIP_H */

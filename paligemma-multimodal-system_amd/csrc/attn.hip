@@ -1,0 +1,265 @@
+// Flash-style attention on MFMA (bf16 in, fp32 softmax/accumulate), no N^2 scores in HBM.
+//
+// Restates the attention cores of SiglipAttention.forward (modeling_siglip.py:96-136,
+// bidirectional, scale 1/sqrt(head_dim)) and GemmaAttention.forward
+// (modeling_gemma.py:307-339: MQA via repeat_kv, scores/sqrt(head_dim) + additive
+// mask, fp32 softmax, P.V) — but the MQA broadcast is free: the q heads that share a
+// kv head are stacked as extra query ROWS of one problem (row r = pos * G + head%G),
+// so one K/V tile feeds all of them.
+//
+// Per wave: 16 query rows.  S^T = K . Q^T (MFMA A = K tile, B = Q fragment) puts one
+// query per lane column, so the online-softmax max/sum are lane-local plus two xor
+// shuffles; O^T = V^T . P^T takes P straight from the S accumulators (the key order
+// inside the k-step is permuted to match, SURVEY/guide 'accumulator as operand') and
+// V^T from a transposed image (Vt[d][key], written transposed by the producer).
+//
+// Modes: normal (prefill): a wave walks all keys and writes normalised bf16 O;
+// split (decode): each wave owns a key range and writes (O, m, l) partials that
+// pg_attn_combine merges.
+#include "common.h"
+
+struct AttnArgs {
+  const bf16_t* q; long q_rs;
+  bf16_t* o; long o_rs;
+  const bf16_t* k; long k_bs, k_hs, k_rs;
+  const bf16_t* vt; long vt_bs, vt_hs, vt_ds;
+  const float* mask; long mask_bs, mask_rs;
+  int Lq, Lkv, G, Hkv, D;
+  const int* lkv_dev;      // if set: Lkv = *lkv_dev + Lkv
+  float scale_log2;        // softmax scale * log2(e)
+  int split_keys;          // split mode if > 0 (keys per wave)
+  float* part_o;           // [B][Hkv][nsplit][16][DT*16]
+  float* part_ml;          // [B][Hkv][nsplit][16][2]
+};
+
+static __device__ __forceinline__ u32x4 ld16_or0(const bf16_t* p, bool ok) {
+  return ok ? *(const u32x4*)p : u32x4{0u, 0u, 0u, 0u};
+}
+
+// 4 consecutive keys of one Vt row, zero beyond kend
+static __device__ __forceinline__ u32x2 ld_vt4(const bf16_t* row, int key, int kend, bool dok) {
+  if (!dok) return u32x2{0u, 0u};
+  if (key + 3 < kend) return *(const u32x2*)(row + key);
+  uint32_t e[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) e[j] = (key + j < kend) ? (uint32_t)row[key + j] : 0u;
+  return u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+}
+
+template <int DP, int DT>
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  constexpr int KS = DP / 32;  // QK^T k-steps
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int c = lane & 15;
+  const int g = lane >> 4;
+  const int b = blockIdx.z;
+  const bool split = a.split_keys > 0;
+  const int nsg = split ? (int)(gridDim.y / a.Hkv) : 1;
+  const int kvh = blockIdx.y / nsg;
+  const int sg = blockIdx.y % nsg;
+  const int Lkv = (a.lkv_dev ? *a.lkv_dev : 0) + a.Lkv;
+  const int R = a.Lq * a.G;
+  const int D = a.D;
+
+  const int r0 = split ? 0 : (blockIdx.x * 64 + wave * 16);
+  int kbeg = 0, kend = Lkv, sp = 0;
+  if (split) {
+    sp = sg * 4 + wave;
+    kbeg = sp * a.split_keys;
+    kend = min(Lkv, kbeg + a.split_keys);
+  }
+  if (!split && r0 >= R) return;
+
+  const int r = r0 + c;
+  const bool rvalid = r < R;
+  const int pos = rvalid ? r / a.G : 0;
+  const int hq = kvh * a.G + (rvalid ? r % a.G : 0);
+
+  bf16x8 qf[KS];
+  {
+    const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int d0 = 32 * s + 8 * g;
+      qf[s] = __builtin_bit_cast(bf16x8, ld16_or0(qp + d0, rvalid && d0 < D));
+    }
+  }
+  const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
+  const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
+  const float* mrow = a.mask ? a.mask + (long)b * a.mask_bs + (long)pos * a.mask_rs : nullptr;
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float LOG2E = 1.4426950408889634f;
+
+  for (int kb = kbeg; kb < kend; kb += 32) {
+    // ---- S^T for keys kb..kb+15 (sA) and kb+16..kb+31 (sB)
+    f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+    {
+      const int ka = kb + c, kbk = kb + 16 + c;
+      const bf16_t* pa = kbase + (long)ka * a.k_rs;
+      const bf16_t* pb = kbase + (long)kbk * a.k_rs;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int d0 = 32 * s + 8 * g;
+        bf16x8 fa = __builtin_bit_cast(bf16x8, ld16_or0(pa + d0, ka < kend && d0 < D));
+        bf16x8 fb = __builtin_bit_cast(bf16x8, ld16_or0(pb + d0, kbk < kend && d0 < D));
+        sA = mfma16(fa, qf[s], sA);
+        sB = mfma16(fb, qf[s], sB);
+      }
+    }
+    // lane holds S[key = kb + 4g + j][q = c] (sA) and S[key = kb + 16 + 4g + j][q = c] (sB)
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k0 = kb + 4 * g + j, k1 = kb + 16 + 4 * g + j;
+      float v0 = sA[j] * a.scale_log2, v1 = sB[j] * a.scale_log2;
+      if (mrow) {
+        if (k0 < kend) v0 += mrow[k0] * LOG2E;
+        if (k1 < kend) v1 += mrow[k1] * LOG2E;
+      }
+      x[j] = k0 < kend ? v0 : -INFINITY;
+      x[4 + j] = k1 < kend ? v1 : -INFINITY;
+    }
+    float bm = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { x[j] = exp2f(x[j] - mn); rs += x[j]; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    // P^T fragment: slot 8g+j <-> key kb+4g+j (j<4), kb+16+4g+(j-4) (j>=4)
+    u32x4 pw;
+    pw[0] = pack_bf2(x[0], x[1]);
+    pw[1] = pack_bf2(x[2], x[3]);
+    pw[2] = pack_bf2(x[4], x[5]);
+    pw[3] = pack_bf2(x[6], x[7]);
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int d = 16 * t + c;
+      const bool dok = d < D;
+      const bf16_t* vrow = vbase + (long)(dok ? d : 0) * a.vt_ds;
+      u32x2 v0 = ld_vt4(vrow, kb + 4 * g, kend, dok);
+      u32x2 v1 = ld_vt4(vrow, kb + 16 + 4 * g, kend, dok);
+      u32x4 vv{v0[0], v0[1], v1[0], v1[1]};
+      o[t] = mfma16(__builtin_bit_cast(bf16x8, vv), pf, o[t]);
+    }
+  }
+
+  // lane holds O^T[d = 16t + 4g + j][q = c]
+  if (!split) {
+    if (!rvalid) return;
+    const float inv = 1.0f / l;
+    bf16_t* op = a.o + ((long)b * a.Lq + pos) * a.o_rs + (long)hq * D;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int d = 16 * t + 4 * g;
+      if (d < D) {
+        u32x2 p;
+        p[0] = pack_bf2(o[t][0] * inv, o[t][1] * inv);
+        p[1] = pack_bf2(o[t][2] * inv, o[t][3] * inv);
+        *(u32x2*)(op + d) = p;
+      }
+    }
+  } else {
+    const int nsplit = nsg * 4;
+    const long base = (((long)b * a.Hkv + kvh) * nsplit + sp) * 16 + c;
+    float* po = a.part_o + base * (DT * 16);
+#pragma unroll
+    for (int t = 0; t < DT; ++t) *(f32x4*)(po + 16 * t + 4 * g) = o[t];
+    if (g == 0) {
+      a.part_ml[base * 2 + 0] = m;
+      a.part_ml[base * 2 + 1] = l;
+    }
+  }
+}
+
+// Merge the split partials: out[b][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s
+__global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
+                                                           const float* __restrict__ part_ml, int nsplit, int G,
+                                                           int Hkv, int D, int DTW, bf16_t* __restrict__ o, long o_rs) {
+  const int bk = blockIdx.x;  // b * Hkv + kvh
+  const int b = bk / Hkv, kvh = bk % Hkv;
+  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
+    const int row = idx / D, d = idx % D;
+    float M = -INFINITY;
+    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[(((long)bk * nsplit + s) * 16 + row) * 2]);
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      const long base = ((long)bk * nsplit + s) * 16 + row;
+      const float ms = part_ml[base * 2];
+      if (ms == -INFINITY) continue;
+      const float f = exp2f(ms - M);
+      num += f * part_o[base * DTW + d];
+      den += f * part_ml[base * 2 + 1];
+    }
+    o[(long)b * o_rs + (long)(kvh * G + row) * D + d] = f2bf(num / den);
+  }
+}
+
+#define ATTN_DISPATCH(DP_, DT_)                                                             \
+  if (DP == DP_ && DT == DT_) {                                                              \
+    hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);              \
+    launched = true;                                                                         \
+  }
+
+// q/o row for (b, pos, head): q + (b*Lq + pos)*q_rs + head*D.  k for (b, key, kvh): k + b*k_bs + kvh*k_hs + key*k_rs.
+// vt for (b, d, key, kvh): vt + b*vt_bs + kvh*vt_hs + d*vt_ds + key.  mask (optional, additive fp32): mask + b*mask_bs
+// + pos*mask_rs + key.  Lkv = (lkv_dev ? *lkv_dev : 0) + Lkv.
+// split_keys == 0: prefill mode (writes bf16 o).  split_keys > 0: decode mode, Lq*Hq/Hkv <= 16, nsplit partials
+// (nsplit multiple of 4) to part_o / part_ml, then call pg_attn_combine.
+extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
+                            long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
+                            long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
+                            int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
+                            hipStream_t stream) {
+  PG_REQUIRE(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && D > 0 && D % 8 == 0 && D <= 256);
+  const int G = Hq / Hkv;
+  const int DP = ((D + 31) / 32) * 32;
+  const int DT = (D + 15) / 16;
+  AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, (const bf16_t*)k, k_bs, k_hs, k_rs,
+             (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, mask, mask_bs, mask_rs,
+             Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml};
+  dim3 grid;
+  if (split_keys > 0) {
+    PG_REQUIRE(Lq * G <= 16 && nsplit % 4 == 0 && part_o && part_ml && split_keys % 32 == 0);
+    grid = dim3(1, Hkv * (nsplit / 4), B);
+  } else {
+    grid = dim3((Lq * G + 63) / 64, Hkv, B);
+  }
+  bool launched = false;
+  ATTN_DISPATCH(32, 1)
+  ATTN_DISPATCH(32, 2)     // head_dim 24 / 32 (test configs)
+  ATTN_DISPATCH(64, 3)
+  ATTN_DISPATCH(64, 4)
+  ATTN_DISPATCH(96, 5)     // SigLIP head_dim 72
+  ATTN_DISPATCH(96, 6)
+  ATTN_DISPATCH(128, 8)
+  ATTN_DISPATCH(256, 16)   // Gemma head_dim 256
+  if (!launched) return (int)hipErrorInvalidValue;
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
+                               void* o, long o_rs, hipStream_t stream) {
+  PG_REQUIRE(Hq % Hkv == 0 && Hq / Hkv <= 16);
+  const int DT = (D + 15) / 16;
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(B * Hkv), dim3(256), 0, stream, part_o, part_ml, nsplit, Hq / Hkv,
+                     Hkv, D, DT * 16, (bf16_t*)o, o_rs);
+  PG_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,257 @@
+"""Generate golden fixtures by running the REFERENCE implementation.
+
+Runs only in the development container, where /root/reference exists; the
+fixtures it writes (tests/golden/*.npz) are data — inputs and the reference's
+outputs — and are what travel.  Nothing here is imported by the product.
+
+Shims:
+  * ``fire`` is not installed -> stub module (inference.py:3 only uses it at :154);
+  * processing_paligemma.py fails to import on Python 3.10 (``List[Image]`` at :38
+    uses the PIL module as a type) -> its unchanged source is compiled with
+    ``from __future__ import annotations`` semantics;
+  * ``Image.show`` (inference.py:21) -> no-op; the reference's prints are silenced.
+
+Weights: oracle/synth.py's name-seeded bf16-exact synthetic tensors, loaded
+with the reference's own ``load_state_dict(strict=False)`` + ``tie_weights``
+(utils.py:33-36).
+
+Usage:  python tests/golden/make_golden.py [tiny] [pt224] [topp]
+"""
+from __future__ import annotations
+
+import __future__
+import contextlib
+import io
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import configs, synth  # noqa: E402
+
+PROMPT_IDS = [2, 651, 4906, 603, 476, 2121, 576, 108]      # <bos> ... "\n"
+TINY_PROMPT_IDS = [2, 65, 120, 33, 250, 17, 9, 108]
+
+
+def import_reference():
+    sys.path.insert(0, REF)
+    sys.modules.setdefault("fire", types.SimpleNamespace(Fire=lambda *a, **k: None))
+    src = open(os.path.join(REF, "processing_paligemma.py")).read()
+    mod = types.ModuleType("processing_paligemma")
+    mod.__file__ = os.path.join(REF, "processing_paligemma.py")
+    code = compile(src, mod.__file__, "exec", flags=__future__.annotations.compiler_flag, dont_inherit=True)
+    exec(code, mod.__dict__)
+    sys.modules["processing_paligemma"] = mod
+    from PIL import Image
+    Image.Image.show = lambda self, *a, **k: None
+    import modeling_paligemma
+    import inference
+    return modeling_paligemma, inference, mod
+
+
+def build_reference_model(mp, cfg: dict):
+    with contextlib.redirect_stdout(io.StringIO()):
+        config = mp.PaliGemmaConfig(**cfg)
+        model = mp.PaliGemmaForConditionalGeneration(config)
+    sd = {k: torch.from_numpy(v) for k, v in synth.generate_state_dict(cfg).items()}
+    res = model.load_state_dict(sd, strict=False)                       # utils.py:33
+    missing = set(res.missing_keys) - {"language_model.lm_head.weight"}
+    assert not missing and not res.unexpected_keys, (missing, res.unexpected_keys)
+    model.tie_weights()                                                  # utils.py:36
+    return model.eval()
+
+
+def synthetic_images(batch: int, size: int, seed: int = 1234) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 256, (batch, size, size, 3), dtype=np.uint8)
+
+
+def pixel_values_via_reference(proc_mod, images_u8: np.ndarray) -> np.ndarray:
+    from PIL import Image
+    size = images_u8.shape[1]
+    out = proc_mod.process_images([Image.fromarray(im) for im in images_u8], size, scale_factor=1 / 255.0,
+                                  resampling=Image.Resampling.BICUBIC)     # processing_paligemma.py:38-73
+    return np.stack(out, axis=0).astype(np.float32)
+
+
+class FakeTokenizer:
+    eos_token_id = 1
+
+    def decode(self, ids, skip_special_tokens=True):
+        ids = ids.reshape(-1).tolist() if hasattr(ids, "reshape") else list(ids)
+        return "|" + ",".join(str(int(i)) for i in ids) + "|"
+
+
+class FakeProcessor:
+    """Stands in for PaliGemmaProcessor: returns fixed tensors (tokenizer absent offline)."""
+
+    def __init__(self, input_ids, pixel_values):
+        self.tokenizer = FakeTokenizer()
+        self._inputs = {"input_ids": torch.from_numpy(input_ids), "pixel_values": torch.from_numpy(pixel_values),
+                        "attention_mask": torch.ones(input_ids.shape, dtype=torch.int64)}
+
+    def __call__(self, text, images):
+        return dict(self._inputs)
+
+
+def run_test_inference(inference, model, input_ids, pixel_values, max_tokens, do_sample=False,
+                       temperature=0.8, top_p=0.9, hook_logits=True):
+    """Drive the reference's own test_inference (inference.py:29-87) and capture
+    generated ids (via the decoded print) and each step's last-position logits."""
+    logits = []
+    handle = None
+    if hook_logits:
+        def hook(mod, inp, out):
+            logits.append(out["logits"][:, -1, :].detach().float().numpy().copy())
+        handle = model.language_model.register_forward_hook(hook)
+    tmp = tempfile.NamedTemporaryFile(suffix=".png", delete=False)
+    from PIL import Image
+    Image.fromarray(np.zeros((8, 8, 3), dtype=np.uint8)).save(tmp.name)
+    buf = io.StringIO()
+    with torch.no_grad(), contextlib.redirect_stdout(buf):
+        inference.test_inference(model, FakeProcessor(input_ids, pixel_values), "cpu", "", tmp.name,
+                                 max_tokens, temperature, top_p, do_sample)
+    os.unlink(tmp.name)
+    if handle is not None:
+        handle.remove()
+    line = [ln for ln in buf.getvalue().splitlines() if ln.startswith("|")][-1]
+    ids = [int(x) for x in line.strip("|").split(",") if x != ""]
+    return ids, logits
+
+
+def topk(x: np.ndarray, k: int = 64):
+    idx = np.argsort(-x, axis=-1, kind="stable")[..., :k]
+    return np.take_along_axis(x, idx, axis=-1), idx
+
+
+def capture_modules(model, n_text_layers):
+    store = {}
+    hs = []
+
+    def mk(name):
+        def h(mod, inp, out):
+            o = out[0] if isinstance(out, tuple) else out
+            store.setdefault(name, o.detach().float().numpy().copy())
+        return h
+    hs.append(model.vision_tower.register_forward_hook(mk("vision_out")))
+    hs.append(model.multi_modal_projector.register_forward_hook(mk("proj_out")))
+    for i in range(n_text_layers):
+        hs.append(model.language_model.model.layers[i].register_forward_hook(mk(f"text_layer_{i}")))
+    hs.append(model.language_model.model.register_forward_hook(mk("text_final_norm")))
+    return store, hs
+
+
+def make_tiny(mp, inference, proc):
+    cfg = configs.TINY
+    model = build_reference_model(mp, cfg)
+    n = configs.num_image_tokens(cfg)
+    size = cfg["vision_config"]["image_size"]
+    out = {}
+    for B in (1, 2):
+        imgs = synthetic_images(B, size)
+        pv = pixel_values_via_reference(proc, imgs)
+        ids = np.array([[cfg["image_token_index"]] * n + TINY_PROMPT_IDS] * B, dtype=np.int64)
+        if B == 2:
+            ids[1, n + 3] = 0                                             # a pad token inside row 1
+        mask = np.ones_like(ids)
+        store, hs = capture_modules(model, cfg["text_config"]["num_hidden_layers"])
+        kv = sys.modules["modeling_gemma"].KVCache()
+        with torch.no_grad(), contextlib.redirect_stdout(io.StringIO()):
+            res = model(input_ids=torch.from_numpy(ids), pixel_values=torch.from_numpy(pv),
+                        attention_mask=torch.from_numpy(mask), kv_cache=kv)
+        for h in hs:
+            h.remove()
+        p = f"b{B}_"
+        out[p + "images_u8"] = imgs
+        out[p + "pixel_values"] = pv
+        out[p + "input_ids"] = ids
+        out[p + "logits"] = res["logits"].float().numpy()
+        out[p + "k_cache0"] = kv.k_cache[0].numpy()
+        out[p + "v_cache0"] = kv.v_cache[-1].numpy()
+        for k, v in store.items():
+            out[p + k] = v
+    # the reference's own loop (greedy), B=1
+    ids = out["b1_input_ids"]
+    gen, logits = run_test_inference(inference, model, ids, out["b1_pixel_values"], 12)
+    out["greedy_ids"] = np.array(gen, dtype=np.int64)
+    out["greedy_logits"] = np.stack(logits, 0)[:, 0]
+    np.savez_compressed(os.path.join(HERE, "tiny.npz"), **out)
+    print("tiny: greedy", gen)
+
+
+def make_pt224(mp, inference, proc, steps=16):
+    cfg = configs.PT_224
+    torch.set_num_threads(os.cpu_count())
+    model = build_reference_model(mp, cfg)
+    n = configs.num_image_tokens(cfg)
+    imgs = synthetic_images(1, 224)
+    pv = pixel_values_via_reference(proc, imgs)
+    ids = np.array([[cfg["image_token_index"]] * n + PROMPT_IDS], dtype=np.int64)
+    store, hs = capture_modules(model, cfg["text_config"]["num_hidden_layers"])
+    gen, logits = run_test_inference(inference, model, ids, pv, steps)
+    for h in hs:
+        h.remove()
+    lg = np.stack(logits, 0)[:, 0]                                        # (steps, V)
+    tv, ti = topk(lg, 64)
+    out = {"images_u8": imgs, "pixel_values": pv, "input_ids": ids,
+           "greedy_ids": np.array(gen, dtype=np.int64), "prefill_last_logits": lg[0],
+           "step_top64_values": tv, "step_top64_ids": ti, "margin": tv[:, 0] - tv[:, 1],
+           "vision_out": store["vision_out"][0], "proj_out_rows": store["proj_out"][0, ::16]}
+    for i in range(cfg["text_config"]["num_hidden_layers"]):
+        h = store[f"text_layer_{i}"][0]
+        out[f"layer_{i}_stats"] = np.array([h.mean(), np.abs(h).max(), np.sqrt((h.astype(np.float64) ** 2).sum())])
+        out[f"layer_{i}_last_row"] = h[-1]
+    out["final_norm_last_row"] = store["text_final_norm"][0, -1]
+    np.savez_compressed(os.path.join(HERE, "pt224.npz"), **out)
+    print("pt224: greedy", gen, "margins", np.round(out["margin"], 3))
+
+
+def make_topp(inference):
+    rng = np.random.default_rng(7)
+    cases = {}
+    for ci, (V, T, P) in enumerate([(257216, 0.8, 0.9), (300, 0.8, 0.9), (4096, 1.3, 0.5), (257216, 0.5, 0.95)]):
+        logits = (rng.standard_normal((1, V)) * 3.0).astype(np.float32)
+        captured = {}
+        real = torch.multinomial
+
+        def fake(probs, num_samples=1, **kw):
+            captured["probs_sort"] = probs.detach().numpy().copy()
+            return torch.zeros((probs.shape[0], num_samples), dtype=torch.int64)
+        torch.multinomial = fake
+        try:
+            probs = torch.softmax(torch.from_numpy(logits) / T, dim=-1)     # inference.py:65
+            idx0 = inference._sample_top_p(probs, P)                        # inference.py:90-106
+        finally:
+            torch.multinomial = real
+        cases[f"c{ci}_logits"] = logits
+        cases[f"c{ci}_T"] = np.float32(T)
+        cases[f"c{ci}_p"] = np.float32(P)
+        ps = captured["probs_sort"][0]
+        keep = int((ps > 0).sum())
+        # the included token set (order-free) and its renormalised probabilities
+        order = torch.sort(probs, dim=-1, descending=True)
+        cases[f"c{ci}_kept_ids"] = order.indices[0, :keep].numpy()
+        cases[f"c{ci}_kept_probs"] = ps[:keep]
+        cases[f"c{ci}_first_idx"] = idx0.numpy()
+    np.savez_compressed(os.path.join(HERE, "topp.npz"), **cases)
+    print("topp: kept sizes", [len(cases[f"c{i}_kept_ids"]) for i in range(4)])
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["tiny", "topp", "pt224"]
+    mp, inference, proc = import_reference()
+    torch.manual_seed(0)
+    if "tiny" in which:
+        make_tiny(mp, inference, proc)
+    if "topp" in which:
+        make_topp(inference)
+    if "pt224" in which:
+        make_pt224(mp, inference, proc)
