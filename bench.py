@@ -1,0 +1,270 @@
+"""Headline bench: PaliGemma-3B image->text tokens/s + prefill ms on MI355X.
+
+A "step" = one full request of BASELINE.json configs[1] (PaliGemma-3B-pt-224, bf16, batch 1,
+greedy): synthetic 224x224 image + 8-token prompt resident in HBM -> SigLIP -> projector ->
+merge -> Gemma prefill -> 128 greedy tokens (graph-replayed decode steps; EOS ignored so the
+token count is fixed).  value = generated tokens / step wall time over all ranks.
+
+Multi-GPU (torch.distributed.run, one rank per GPU): --parallel dp (default) runs one request per
+rank (independent replicas, weak scaling); value = all ranks' tokens / max-over-ranks time.
+
+Extra fields: prefill_ms, decode_tok_s, decode HBM fraction; "roofline" for the dominant
+kernel (the decode gate/up GEMV, HIP events on the stream it runs on); "cpu_baseline" = the
+oracle (numpy port of the reference path, fp32, vision re-run per token as the reference does)
+on a bounded sample, rank 0, N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "paligemma-multimodal-system_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFS = 2500.0     # dense bf16 MFMA
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_inputs(cfg, B, prompt_ids):
+    from pghip.configs import num_image_tokens
+    n = num_image_tokens(cfg)
+    size = cfg["vision_config"].get("image_size", 224)
+    rng = np.random.default_rng(1234)
+    img = rng.integers(0, 256, (B, size, size, 3), dtype=np.uint8)
+    px = ((img.astype(np.float32) * np.float32(1 / 255.0)) - np.float32(0.5)) / np.float32(0.5)
+    px = torch.from_numpy(np.ascontiguousarray(px.transpose(0, 3, 1, 2)))
+    ids = torch.tensor([[cfg["image_token_index"]] * n + prompt_ids] * B, dtype=torch.int64)
+    return ids, px
+
+
+def prefill_flops(cfg, B, L):
+    """sum 2*M*N*K over linears + attention + last-token lm_head."""
+    v, t = cfg["vision_config"], cfg["text_config"]
+    n = (v.get("image_size", 224) // v["patch_size"]) ** 2
+    hv, iv, lv = v["hidden_size"], v["intermediate_size"], v["num_hidden_layers"]
+    vis = 2 * n * (3 * 14 * 14) * hv + lv * (2 * n * hv * hv * 4 + 2 * n * hv * iv * 2 + 4 * n * n * hv)
+    vis += 2 * n * hv * cfg.get("projection_dim", 2048)
+    H, I, nh, nkv, hd = t["hidden_size"], t["intermediate_size"], t["num_attention_heads"], t["num_key_value_heads"], 256
+    per = 2 * L * H * (nh * hd + 2 * nkv * hd) + 2 * L * nh * hd * H + 2 * L * H * I * 3 + 4 * L * L * nh * hd
+    txt = t["num_hidden_layers"] * per + 2 * H * t["vocab_size"]
+    return B * (vis + txt)
+
+
+def time_dominant_kernel(eng, reps=50):
+    """Average duration of the decode gate/up GEMV (the largest byte stream of a decode step) with HIP
+    events on the current stream, which is the stream it is launched on."""
+    from pghip import ops
+    w = eng.w
+    L0 = w.tl[0]
+    x = torch.randn(1, w.hidden, device="cuda").to(torch.bfloat16)
+    h = torch.empty(1, w.inter, dtype=torch.bfloat16, device="cuda")
+    for _ in range(5):
+        ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+    # rotate over the 18 layers' weights so every launch streams from HBM (no L2/MALL reuse)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    ev0.record()
+    for i in range(reps):
+        ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+    ev1.record()
+    torch.cuda.synchronize()
+    avg_s = ev0.elapsed_time(ev1) / 1e3 / reps
+    nbytes = L0["gu_w"].numel() * 2 + w.hidden * 2 + w.inter * 2
+    return avg_s, nbytes
+
+
+def cpu_baseline(cfg, ids, px, budget_tokens=3):
+    """The oracle (numpy fp32 port of the reference path) on the host: one request of the same workload,
+    bounded to `budget_tokens` generated tokens (prefill + decode steps, vision re-run per call as the
+    reference's modeling_paligemma.py:281 does).  Weights: the same synthetic tensors, copied from HBM."""
+    from oracle import paligemma_oracle as O
+    from pghip import synthetic
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([p.get("num_threads", 1) for p in threadpool_info() if p.get("user_api") == "blas"] or [1])
+    except Exception:
+        threads = os.cpu_count()
+    sd = synthetic.SyntheticStateDict(cfg)
+    W = {k: sd[k].float().cpu().numpy() for k in sd.keys()}
+    torch.cuda.empty_cache()
+    orc = O.PaliGemmaOracle(cfg, W, recompute_vision=True)
+    t0 = time.perf_counter()
+    out = O.generate(orc, ids.numpy(), px.numpy(), np.ones_like(ids.numpy()), budget_tokens, stop_token=None)
+    dt = time.perf_counter() - t0
+    del W, orc
+    return {"value": round(len(out) * ids.shape[0] / dt, 4), "unit": "tokens/s", "cores": int(threads),
+            "kind": "port",
+            "sample": f"{len(out)} generated tokens of the same request (1 prefill L={ids.shape[1]} + "
+                      f"{len(out) - 1} decode steps re-running SigLIP like the reference), fp32 numpy, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="pt-224")
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--gen-tokens", type=int, default=128)
+    ap.add_argument("--parallel", default="dp", choices=["dp"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from pghip import configs, engine, synthetic, weights
+    cfg = configs.CONFIGS[args.config]
+    B, T = args.batch, args.gen_tokens
+    t0 = time.perf_counter()
+    sd = synthetic.SyntheticStateDict(cfg)
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+    torch.cuda.synchronize()
+    log(f"[bench] rank {rank}: weights generated+packed in {time.perf_counter() - t0:.1f}s "
+        f"({eng.w.nbytes() / 1e9:.2f} GB)")
+    prompt = [2, 651, 4906, 603, 476, 2121, 576, 108]
+    ids_cpu, px_cpu = synthetic_inputs(cfg, B, prompt)
+    ids, px = ids_cpu.cuda(), px_cpu.cuda()
+    mask = torch.ones_like(ids)
+    L = ids.shape[1]
+
+    # one request = prefill + T-1 graph-replayed decode steps (first token comes from the prefill)
+    state = {}
+
+    def setup():
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, mask, T)
+        st = eng.decode_state(B, cache, nxt, T)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        state.update(cache=cache, feats=feats, st=st)
+        return st
+
+    st = setup()
+    replay = eng._graph_step(st, state["cache"], state["feats"], dict(do_sample=False))
+    graph_cache = state["cache"]
+
+    def request():
+        # prefill into the graph's static cache / state, then replay the captured decode step
+        feats = eng.vision(px)
+        resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
+        eng.embed_merge(ids, feats, resid)
+        pos = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
+        rows = eng._buf("p_rows", (B,), torch.int32)
+        logits, _ = eng.gemma_prefill(resid, pos, graph_cache, B, L, logits_rows=rows)
+        state["st"]["pos"].fill_(L + 1)
+        state["st"]["kv_len"].fill_(L)
+        state["st"]["step"].zero_()
+        state["feats"].copy_(feats)
+        eng.sample(logits, state["st"], dict(do_sample=False), advance=False)
+        for _ in range(T - 1):
+            replay()
+
+    rows = eng._buf("p_rows", (B,), torch.int32)
+    rows.copy_(torch.arange(B, dtype=torch.int32) * L + (L - 1))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        request()
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        request()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        tt = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    ms_per_step = elapsed / args.steps * 1e3
+    tokens = B * T * args.steps * world
+    value = tokens / elapsed
+
+    # prefill-only and decode-only timings (same stream, events)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    for _ in range(3):
+        feats = eng.vision(px)
+        resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
+        eng.embed_merge(ids, feats, resid)
+        pos = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
+        eng.gemma_prefill(resid, pos, graph_cache, B, L, logits_rows=rows)
+    ev[1].record()
+    state["st"]["kv_len"].fill_(L)
+    state["st"]["pos"].fill_(L + 1)
+    ev[2].record()
+    for _ in range(T - 1):
+        replay()
+    ev[3].record()
+    torch.cuda.synchronize()
+    prefill_ms = ev[0].elapsed_time(ev[1]) / 3
+    decode_ms_tok = ev[2].elapsed_time(ev[3]) / (T - 1)
+    step_bytes = eng.w.decode_weight_bytes()
+    kv_bytes = B * (L + T // 2) * eng.w.t_layers * 2 * eng.w.kv_heads * eng.w.head_dim * 2
+    decode_hbm = (step_bytes + kv_bytes) / (decode_ms_tok / 1e3) / 1e9
+    pf_flops = prefill_flops(cfg, B, L)
+
+    kern_s, kern_bytes = time_dominant_kernel(eng)
+    achieved = kern_bytes / kern_s / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del state, eng
+        torch.cuda.empty_cache()
+        try:
+            cpu = cpu_baseline(cfg, ids_cpu, px_cpu)
+        except Exception as e:  # report, do not fail the bench
+            cpu = {"value": None, "unit": "tokens/s", "cores": os.cpu_count(), "kind": "port", "sample": f"failed: {e}"}
+
+    if rank == 0:
+        rec = {
+            "metric": "image->text tokens/s (PaliGemma-3B-224, greedy, 128 new tokens) + prefill ms",
+            "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights of the "
+            "PaliGemma-3B architecture, name-seeded; random 224x224 image; 8-token prompt)",
+            "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
+                                   f"{T} greedy tokens (BASELINE.json configs[1])",
+                       "global_batch": B * world, "seq_len": L + T, "parallelism": f"dp{world}"},
+            "prefill_ms": round(prefill_ms, 3),
+            "prefill_tflops": round(pf_flops / (prefill_ms / 1e3) / 1e12, 2),
+            "prefill_mfma_frac": round(pf_flops / (prefill_ms / 1e3) / 1e12 / BF16_PEAK_TFS, 4),
+            "decode_ms_per_token": round(decode_ms_tok, 4),
+            "decode_tok_s": round(B / (decode_ms_tok / 1e3), 1),
+            "decode_hbm_gbs": round(decode_hbm, 1),
+            "decode_hbm_frac": round(decode_hbm / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gemv_kernel<GELU_MUL,2> (decode gate/up, 2x16384x2048 bf16)",
+                         "kernel_avg_us": round(kern_s * 1e6, 2), "bytes_per_launch": kern_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,73 @@
+"""ctypes binding of libpghip.so (the C-ABI declared in include/pghip.h).
+
+There is no fallback: if the library is missing or a call fails, this raises.
+Import torch before loading so the HIP runtime torch ships is the one the library
+binds to (same soname, libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpghip.so")
+
+vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
+
+# name -> argtypes (every function returns int: 0 or a hipError_t code)
+SIGNATURES = {
+    "pg_abi_version": [],
+    "pg_gemm": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp],
+    "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
+    "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
+                     i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, vp],
+    "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
+    "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],
+    "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],
+    "pg_image_rank": [vp, i32, i64, vp, vp],
+    "pg_embed_merge": [vp, vp, i32, vp, i32, vp, i32, i32, i64, i64, f32, f32, vp, vp],
+    "pg_argmax": [vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp],
+    "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp],
+    "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
+}
+
+_lib = None
+_hip = None
+
+
+class PgHipError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PgHipError(f"libpghip.so not found at {path}: build it with `python -m pghip.build` "
+                         "(or __graft_entry__.build()); there is no CPU fallback.")
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = C.c_int
+    _lib = lib
+    return lib
+
+
+def _err_string(code: int) -> str:
+    global _hip
+    try:
+        if _hip is None:
+            _hip = C.CDLL("libamdhip64.so.7")
+            _hip.hipGetErrorString.restype = C.c_char_p
+            _hip.hipGetErrorString.argtypes = [C.c_int]
+        return _hip.hipGetErrorString(code).decode()
+    except Exception:  # pragma: no cover
+        return "?"
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise PgHipError(f"{name} failed: hip error {rc} ({_err_string(rc)})")

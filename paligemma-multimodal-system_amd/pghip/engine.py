@@ -1,0 +1,331 @@
+"""PaliGemma image->text engine on libpghip (one process per GPU).
+
+Restates PaliGemmaForConditionalGeneration.forward (modeling_paligemma.py:257-308)
+and the test_inference token loop (inference.py:45-82) as a fixed sequence of
+HIP kernels:
+
+  vision (once per request)  im2col -> patch GEMM(+bias+pos) -> 27 x [LN -> QKV GEMM(+bias, V^T)
+                             -> attention -> out GEMM(split-K partials) -> LN(+partials) -> fc1 GEMM(+gelu)
+                             -> fc2 GEMM(partials)] -> post-LN -> projector GEMM
+  prefill                    rank scan -> embed merge -> 18 x [RMSNorm(+partials) -> QKV GEMM -> RoPE+KV write
+                             -> attention -> o GEMM(partials) -> RMSNorm -> gate/up GEMM(gelu*mul) -> down GEMM
+                             (partials)] -> final RMSNorm -> lm_head GEMM(+bias)
+  decode step                the same per token with the GEMV kernels, split-KV attention, argmax / top-p;
+                             every per-step scalar (kv length, positions, step) lives in device memory,
+                             so one step is captured once as a hipGraph and replayed.
+
+Output-invariant deviations from the reference: the vision
+tower runs once per request instead of on every call (modeling_paligemma.py:281);
+the KV cache is a static in-place buffer instead of torch.cat (modeling_gemma.py:54-55);
+the generation loop computes only last-position logits.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import ops
+from .weights import PackedWeights
+
+
+def _rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def rope_tables(dim: int, n_pos: int, base: float, device):
+    """cos/sin [n_pos][dim/2] exactly as GemmaRotaryEmbedding (modeling_gemma.py:112,121-135):
+    inv_freq = 1/base^(arange(0,dim,2)/dim) in fp32, freqs = inv_freq * pos (fp32), cos/sin in fp32.
+    Computed with torch on the CPU (the reference's own arithmetic), then uploaded."""
+    inv = 1.0 / (base ** (torch.arange(0, dim, 2, dtype=torch.int64).float() / dim))
+    pos = torch.arange(n_pos, dtype=torch.int64).float()
+    freqs = inv[None, :] * pos[:, None]
+    return freqs.cos().to(device).contiguous(), freqs.sin().to(device).contiguous()
+
+
+class KVStore:
+    """Static KV cache: K [layers][B][Smax][nkv*hd] (roped), V^T [layers][B][nkv*hd][Smax], bf16."""
+
+    def __init__(self, layers: int, B: int, Smax: int, kv_dim: int, device):
+        self.B, self.Smax, self.kv_dim = B, Smax, kv_dim
+        self.k = torch.zeros(layers, B, Smax, kv_dim, dtype=torch.bfloat16, device=device)
+        self.vt = torch.zeros(layers, B, kv_dim, Smax, dtype=torch.bfloat16, device=device)
+        self.length = 0
+
+
+class PaliGemmaEngine:
+    DECODE_SPLIT_O = 2      # split-K of o_proj at decode (partials reduced by the next RMSNorm)
+    DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
+    DECODE_SPLIT_KEYS = 64  # keys per wave in split-KV decode attention
+
+    def __init__(self, cfg: dict, weights: PackedWeights, device="cuda"):
+        self.cfg = cfg
+        self.w = weights
+        self.device = torch.device(device)
+        self.image_token_id = cfg["image_token_index"]
+        pad = cfg.get("pad_token_id")
+        self.pad_id = -1 if pad is None else pad
+        self.n_img = weights.n_img
+        self._rope = None
+        self._rope_n = 0
+        self._ws = {}
+        self.graphs = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _buf(self, name, shape, dtype):
+        t = self._ws.get(name)
+        n = math.prod(shape)
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(max(n, 1), dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:n].view(*shape)
+
+    def rope(self, n_pos: int):
+        if self._rope is None or self._rope_n < n_pos:
+            n = _rup(max(n_pos, 1024), 1024)
+            self._rope = rope_tables(self.w.head_dim, n, self.w.rope_theta, self.device)
+            self._rope_n = n
+        return self._rope
+
+    def new_cache(self, B: int, Smax: int) -> KVStore:
+        w = self.w
+        return KVStore(w.t_layers, B, _rup(Smax, 64), w.kv_heads * w.head_dim, self.device)
+
+    # ------------------------------------------------------------------ vision tower
+    def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False):
+        """SiglipVisionModel.forward + projector (modeling_siglip.py:312-334, modeling_paligemma.py:60-65).
+        Returns image features fp32 [B*N][P] (projector output, unscaled) and optionally the
+        post-LN vision output fp32 [B*N][hv]."""
+        w = self.w
+        px = pixel_values.to(device=self.device, dtype=torch.float32).contiguous()
+        B = px.shape[0]
+        N, hv, nh, hd = w.n_img, w.v_hidden, w.v_heads, w.v_head_dim
+        M = B * N
+        patches = self._buf("v_patches", (M, w.patch_k), torch.bfloat16)
+        ops.patch_im2col(px, w.patch, patches)
+        resid = self._buf("v_resid", (M, hv), torch.float32)
+        ops.gemm(patches, w.patch_w, resid, epi=ops.EPI_F32_POS, bias=w.patch_b, aux=w.pos_emb, aux_rows=N)
+        xn = self._buf("v_xn", (M, hv), torch.bfloat16)
+        qkv = self._buf("v_qkv", (M, 3 * hv), torch.bfloat16)
+        vt = self._buf("v_vt", (hv, M), torch.bfloat16)
+        attn = self._buf("v_attn", (M, hv), torch.bfloat16)
+        h = self._buf("v_h", (M, w.v_inter), torch.bfloat16)
+        tiles = lambda n: ((M + 127) // 128) * ((n + 127) // 128)  # noqa: E731
+        s_o = ops.split_for(tiles(hv), hv // 64)
+        s_2 = ops.split_for(tiles(hv), w.v_inter // 64)
+        part = self._buf("v_part", (max(s_o, s_2), M, hv), torch.float32)
+        ns = 0
+        for L in w.vl:
+            ops.norm_residual(resid, L["ln1_w"], b=L["ln1_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
+                              nsplit=ns, out=xn)
+            ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M, aux_n=2 * hv)
+            ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * M, M,
+                          B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5))
+            ops.gemm(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
+            ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
+                              nsplit=s_o, out=xn)
+            ops.gemm(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"])
+            ops.gemm(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
+            ns = s_2
+        hid = torch.empty(M, hv, dtype=torch.float32, device=self.device) if want_hidden else None
+        ops.norm_residual(resid, w.post_w, b=w.post_b, mode=ops.NORM_LAYER, eps=w.v_eps, partials=part, nsplit=ns,
+                          out=xn, out_f32=hid)
+        feats = torch.empty(M, w.proj_dim, dtype=torch.float32, device=self.device)
+        ops.gemm(xn, w.proj_w, feats, epi=ops.EPI_F32)
+        return (feats, hid) if want_hidden else feats
+
+    # ------------------------------------------------------------------ Gemma stack (prefill, T = B*L rows)
+    def embed_merge(self, input_ids: torch.Tensor, feats: torch.Tensor, out: torch.Tensor, rank=None):
+        w = self.w
+        ids = input_ids.reshape(-1)
+        n = ids.numel()
+        if rank is None and n > 64:
+            rank = self._buf("rank", (n,), torch.int32)
+            ops.image_rank(ids, self.image_token_id, rank)
+        ops.embed_merge(ids, rank, w.embed, feats, feats.shape[0] if feats is not None else 0, out,
+                        image_id=self.image_token_id, pad_id=self.pad_id,
+                        img_scale=float(w.proj_dim ** -0.5), normalizer=float(w.hidden ** 0.5))
+
+    def gemma_prefill(self, x_resid: torch.Tensor, positions: torch.Tensor, cache: KVStore, B: int, L: int,
+                      logits_rows: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
+                      want_hidden: bool = False, want_logits: bool = True):
+        """GemmaForCausalLM.forward after the *sqrt(H) (modeling_gemma.py:510-534) on resid fp32 [B*L][H]
+        (already scaled).  Fills cache slots [0, L).  logits_rows: int32 rows to emit logits for (None = all)."""
+        w = self.w
+        T = B * L
+        H, I, nh, nkv, hd = w.hidden, w.inter, w.heads, w.kv_heads, w.head_dim
+        cos_t, sin_t = self.rope(L + 2)
+        xn = self._buf("t_xn", (T, H), torch.bfloat16)
+        qkv = self._buf("t_qkv", (T, w.qkv_n), torch.bfloat16)
+        attn = self._buf("t_attn", (T, nh * hd), torch.bfloat16)
+        h = self._buf("t_h", (T, I), torch.bfloat16)
+        tiles = lambda n: ((T + 127) // 128) * ((n + 127) // 128)  # noqa: E731
+        s_o = ops.split_for(tiles(H), (nh * hd) // 64) if T > 16 else self.DECODE_SPLIT_O
+        s_d = ops.split_for(tiles(H), I // 64) if T > 16 else self.DECODE_SPLIT_DOWN
+        part = self._buf("t_part", (max(s_o, s_d), T, H), torch.float32)
+        pos = positions.to(device=self.device, dtype=torch.int32).reshape(-1).contiguous()
+        ns = 0
+        kvd = nkv * hd
+        for i, Lw in enumerate(w.tl):
+            ops.norm_residual(x_resid, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            ops.gemm(xn, Lw["qkv_w"], qkv)
+            ops.rope_kv_write(qkv, pos, cos_t, sin_t, cache.k[i], cache.vt[i], T=T, L=L, Hq=nh, Hkv=nkv, D=hd,
+                              Smax=cache.Smax)
+            ops.attention(qkv, w.qkv_n, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
+                          mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
+                          mask_rs=(mask.stride(-2) if mask is not None else 0))
+            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=s_o)
+            ops.norm_residual(x_resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=s_o, out=xn)
+            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=s_d)
+            ns = s_d
+        cache.length = L
+        rows = logits_rows.numel() if logits_rows is not None else T
+        xf = self._buf("t_xf", (rows, H), torch.bfloat16)
+        hid = torch.empty(rows, H, dtype=torch.float32, device=self.device) if want_hidden else None
+        ops.norm_residual(x_resid, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xf, out_f32=hid,
+                          row_map=logits_rows, write_resid=False)
+        logits = None
+        if want_logits:
+            logits = torch.empty(rows, w.vocab, dtype=torch.float32, device=self.device)
+            ops.gemm(xf, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
+        return logits, hid
+
+    # ------------------------------------------------------------------ decode step (graph-capturable)
+    def decode_state(self, B: int, cache: KVStore, positions_next: torch.Tensor, max_steps: int):
+        """Device-resident decode state: ids, positions, kv length, step counter, token history."""
+        st = {
+            "ids": torch.zeros(B, dtype=torch.int64, device=self.device),
+            "pos": positions_next.to(device=self.device, dtype=torch.int32).reshape(B).contiguous().clone(),
+            "kv_len": torch.full((1,), cache.length, dtype=torch.int32, device=self.device),
+            "step": torch.zeros(1, dtype=torch.int32, device=self.device),
+            "hist": torch.zeros(max_steps + 1, B, dtype=torch.int64, device=self.device),
+            "ws": torch.empty(B * 64 * 2, dtype=torch.float32, device=self.device),
+        }
+        return st
+
+    def decode_step(self, st: dict, cache: KVStore, feats: Optional[torch.Tensor], sampler: dict):
+        """One token for B rows: embed(ids) -> 18 layers -> lm_head -> argmax/top-p (advances the state)."""
+        w = self.w
+        B = st["ids"].numel()
+        H, I, nh, nkv, hd = w.hidden, w.inter, w.heads, w.kv_heads, w.head_dim
+        kvd = nkv * hd
+        cos_t, sin_t = self.rope(cache.Smax + 2)
+        resid = self._buf("d_resid", (B, H), torch.float32)
+        xn = self._buf("d_xn", (B, H), torch.bfloat16)
+        qkv = self._buf("d_qkv", (B, w.qkv_n), torch.bfloat16)
+        attn = self._buf("d_attn", (B, nh * hd), torch.bfloat16)
+        h = self._buf("d_h", (B, I), torch.bfloat16)
+        part = self._buf("d_part", (max(self.DECODE_SPLIT_O, self.DECODE_SPLIT_DOWN), B, H), torch.float32)
+        SK = self.DECODE_SPLIT_KEYS
+        nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
+        dt = (hd + 15) // 16 * 16
+        part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
+        part_ml = self._buf("d_pml", (B * nkv * nsplit * 16 * 2,), torch.float32)
+        logits = self._buf("d_logits", (B, w.vocab), torch.float32)
+        ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, resid,
+                        image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
+                        normalizer=float(w.hidden ** 0.5))
+        ns = 0
+        for i, Lw in enumerate(w.tl):
+            ops.norm_residual(resid, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            ops.gemm(xn, Lw["qkv_w"], qkv)
+            ops.rope_kv_write(qkv, st["pos"], cos_t, sin_t, cache.k[i], cache.vt[i], T=B, L=1, Hq=nh, Hkv=nkv,
+                              D=hd, Smax=cache.Smax, slot_dev=st["kv_len"])
+            ops.attention(qkv, w.qkv_n, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
+            ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=self.DECODE_SPLIT_O)
+            ops.norm_residual(resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=self.DECODE_SPLIT_O,
+                              out=xn)
+            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=self.DECODE_SPLIT_DOWN)
+            ns = self.DECODE_SPLIT_DOWN
+        ops.norm_residual(resid, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+        ops.gemm(xn, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
+        self.sample(logits, st, sampler, advance=True)
+        return logits
+
+    def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool):
+        kw = dict(hist=st["hist"], step=st["step"])
+        if advance:
+            kw.update(pos=st["pos"], kv_len=st["kv_len"])
+        if sampler.get("do_sample"):
+            ops.topp_sample(logits, st["ids"], sampler["uniforms"], temperature=sampler["temperature"],
+                            top_p=sampler["top_p"], **kw)
+        else:
+            ops.argmax(logits, st["ids"], st["ws"], **kw)
+
+    # ------------------------------------------------------------------ full request
+    def prefill_request(self, input_ids: torch.Tensor, pixel_values: torch.Tensor, attention_mask: torch.Tensor,
+                        max_new_tokens: int, feats: Optional[torch.Tensor] = None):
+        """Vision + merge + Gemma prefill; returns (cache, feats, last-position logits [B][V], next positions)."""
+        B, L = input_ids.shape
+        if feats is None:
+            feats = self.vision(pixel_values)
+        cache = self.new_cache(B, L + max_new_tokens + 1)
+        resid = self._buf("p_resid", (B * L, self.w.hidden), torch.float32)
+        self.embed_merge(input_ids.to(self.device), feats, resid)
+        am = attention_mask.to(self.device)
+        pos = am.cumsum(-1).masked_fill(am == 0, 1)                       # modeling_paligemma.py:195
+        rows = (torch.arange(B, device=self.device, dtype=torch.int32) * L + (L - 1)).contiguous()
+        logits, _ = self.gemma_prefill(resid, pos, cache, B, L, logits_rows=rows)
+        nxt = am.sum(-1).to(torch.int32) + 1                              # modeling_paligemma.py:189
+        return cache, feats, logits, nxt
+
+    def generate(self, input_ids, pixel_values, attention_mask, max_new_tokens: int, do_sample=False,
+                 temperature=0.8, top_p=0.9, uniforms=None, stop_token: Optional[int] = 1, use_graph=True,
+                 check_every: int = 1):
+        """test_inference's loop (inference.py:45-82): returns generated ids [B][n] (stops at EOS for B=1)."""
+        B = input_ids.shape[0]
+        cache, feats, logits, nxt = self.prefill_request(input_ids, pixel_values, attention_mask, max_new_tokens)
+        st = self.decode_state(B, cache, nxt, max_new_tokens)
+        sampler = dict(do_sample=do_sample, temperature=temperature, top_p=top_p)
+        if do_sample:
+            if uniforms is None:
+                uniforms = torch.rand(max_new_tokens + 1, B)
+            sampler["uniforms"] = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
+        self.sample(logits, st, sampler, advance=False)                  # token 1 from the prefill logits
+        n = 1
+        step_fn = self._graph_step(st, cache, feats, sampler) if use_graph else \
+            (lambda: self.decode_step(st, cache, feats, sampler))
+        while n < max_new_tokens:
+            if stop_token is not None and B == 1 and (n % check_every == 0):
+                if int(st["ids"][0]) == stop_token:                       # inference.py:73-74
+                    break
+            step_fn()
+            n += 1
+        hist = st["hist"][:n].t().contiguous().cpu()
+        if stop_token is not None and B == 1:
+            row = hist[0].tolist()
+            if stop_token in row:
+                row = row[: row.index(stop_token) + 1]
+            return torch.tensor([row], dtype=torch.int64)
+        return hist
+
+    def _graph_step(self, st, cache, feats, sampler):
+        """Capture one decode step into a hipGraph (warm-up run first, on a side stream)."""
+        torch.cuda.synchronize()
+        # warm-up pass to allocate every workspace outside capture, then undo its state advance
+        snap = {k: st[k].clone() for k in ("ids", "pos", "kv_len", "step")}
+        hist0 = st["hist"].clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.decode_step(st, cache, feats, sampler)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for k, v in snap.items():
+            st[k].copy_(v)
+        st["hist"].copy_(hist0)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.decode_step(st, cache, feats, sampler)
+        torch.cuda.synchronize()
+        self.graphs["decode"] = g
+        return g.replay

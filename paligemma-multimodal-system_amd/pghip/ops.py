@@ -1,0 +1,144 @@
+"""Tensor-level wrappers over the C-ABI (include/pghip.h).
+
+Every function takes CUDA(HIP) torch tensors, checks dtype/shape/contiguity on
+the host (so no kernel is launched with a shape it does not handle), and
+enqueues on torch's current stream.  torch is used only for memory and streams.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT = range(6)
+NORM_LAYER, NORM_RMS = 0, 1
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(t: torch.Tensor, dtype, name: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"pghip: {name} must be on the HIP device (got {t.device}); no CPU path")
+    if t.dtype != dtype:
+        raise TypeError(f"pghip: {name} must be {dtype}, got {t.dtype}")
+
+
+def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_BF16,
+         bias: Optional[torch.Tensor] = None, ksplit: int = 1, N: Optional[int] = None,
+         aux: Optional[torch.Tensor] = None, aux_rows: int = 0, aux_out: Optional[torch.Tensor] = None,
+         aux_ld: int = 0, aux_n: int = 0, M: Optional[int] = None) -> torch.Tensor:
+    """out = epilogue(A[M][K] . W[N][K]^T).  K = W.shape[1] (zero-padded), A.shape[1] >= K."""
+    _chk(A, torch.bfloat16, "A")
+    _chk(W, torch.bfloat16, "W")
+    if A.stride(1) != 1 or W.stride(1) != 1 or out.stride(-1) != 1:
+        raise ValueError("pghip.gemm: inner dims must be contiguous")
+    M = A.shape[0] if M is None else M
+    N = W.shape[0] if N is None else N
+    K = W.shape[1]
+    if A.shape[1] < K:
+        raise ValueError(f"pghip.gemm: A has {A.shape[1]} cols < K={K}")
+    if bias is not None:
+        _chk(bias, torch.float32, "bias")
+    ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
+    if epi == EPI_F32:
+        _chk(out, torch.float32, "out")
+        need = ksplit * M * ldc
+        if out.numel() < need:
+            raise ValueError("pghip.gemm: partial output too small")
+    elif epi == EPI_F32_POS:
+        _chk(out, torch.float32, "out")
+    else:
+        _chk(out, torch.bfloat16, "out")
+    if M > 16 and K % 64:
+        raise ValueError("pghip.gemm: K must be a multiple of 64 for M > 16")
+    _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
+              _p(aux), aux_rows, _p(aux_out), aux_ld, aux_n, _s())
+    return out
+
+
+def norm_residual(resid: torch.Tensor, w: torch.Tensor, *, b: Optional[torch.Tensor] = None,
+                  mode: int = NORM_RMS, eps: float = 1e-6, partials: Optional[torch.Tensor] = None,
+                  nsplit: int = 0, out: Optional[torch.Tensor] = None, out_f32: Optional[torch.Tensor] = None,
+                  row_map: Optional[torch.Tensor] = None, write_resid: bool = True):
+    _chk(resid, torch.float32, "resid")
+    M, H = resid.shape[-2], resid.shape[-1]
+    M_out = row_map.numel() if row_map is not None else M
+    ldo = out.stride(-2) if out is not None else H
+    _lib.call("pg_norm_residual", _p(resid), _p(partials), nsplit, M, _p(w), _p(b), _p(out), ldo, _p(out_f32),
+              _p(row_map), M_out, H, mode, float(eps), int(write_resid), _s())
+
+
+def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lq, Lkv, Hq, Hkv, D,
+              scale, mask=None, mask_bs=0, mask_rs=0, lkv_dev=None, split_keys=0, nsplit=0, part_o=None,
+              part_ml=None):
+    """q/k/vt/o are base tensors (bf16) with explicit element strides (see include/pghip.h)."""
+    _lib.call("pg_attention", _p(q), q_rs, _p(o), o_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds,
+              _p(mask), mask_bs, mask_rs, B, Lq, Lkv, _p(lkv_dev), Hq, Hkv, D, float(scale), split_keys, nsplit,
+              _p(part_o), _p(part_ml), _s())
+
+
+def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
+    _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
+
+
+def rope_kv_write(qkv, pos, cos_t, sin_t, kc, vtc, *, T, L, Hq, Hkv, D, Smax, slot_base=0, slot_dev=None):
+    _chk(qkv, torch.bfloat16, "qkv")
+    _chk(pos, torch.int32, "pos")
+    _lib.call("pg_rope_kv_write", _p(qkv), qkv.stride(0), _p(pos), T, L, Hq, Hkv, D, _p(cos_t), _p(sin_t), _p(kc),
+              _p(vtc), Smax, slot_base, _p(slot_dev), _s())
+
+
+def patch_im2col(px: torch.Tensor, patch: int, out: torch.Tensor):
+    _chk(px, torch.float32, "pixel_values")
+    px = px.contiguous()
+    B, C, H, W = px.shape
+    _lib.call("pg_patch_im2col", _p(px), B, C, H, W, patch, _p(out), out.stride(0), _s())
+
+
+def image_rank(ids: torch.Tensor, image_id: int, rank: torch.Tensor):
+    _chk(ids, torch.int64, "input_ids")
+    _lib.call("pg_image_rank", _p(ids), ids.numel(), int(image_id), _p(rank), _s())
+
+
+def embed_merge(ids, rank, embed, feat, n_feat, out, *, image_id, pad_id, img_scale, normalizer):
+    _chk(ids, torch.int64, "input_ids")
+    V, H = embed.shape
+    _lib.call("pg_embed_merge", _p(ids), _p(rank), ids.numel(), _p(embed), V, _p(feat), n_feat, H, int(image_id),
+              int(pad_id), float(img_scale), float(normalizer), _p(out), _s())
+
+
+def argmax(logits, out_ids, workspace, *, hist=None, step=None, pos=None, kv_len=None):
+    _chk(logits, torch.float32, "logits")
+    B, V = logits.shape
+    _lib.call("pg_argmax", _p(logits), logits.stride(0), B, V, _p(workspace), _p(out_ids), _p(hist), _p(step),
+              _p(pos), _p(kv_len), _s())
+
+
+def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, step=None, pos=None, kv_len=None,
+                probs_out=None):
+    _chk(logits, torch.float32, "logits")
+    B, V = logits.shape
+    _lib.call("pg_topp_sample", _p(logits), logits.stride(0), B, V, float(temperature), float(top_p), _p(uniforms),
+              _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
+
+
+def synth_fill(out: torch.Tensor, seedmix: int, a: float, mean: float):
+    kind = 0 if out.dtype == torch.bfloat16 else 1
+    if kind == 1:
+        _chk(out, torch.float32, "out")
+    _lib.call("pg_synth_fill", _p(out), out.numel(), seedmix & 0xFFFFFFFF, float(a), float(mean), kind, _s())
+
+
+def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 16) -> int:
+    """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
+    s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))
+    return s

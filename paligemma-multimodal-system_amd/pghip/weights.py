@@ -1,0 +1,129 @@
+"""Pack reference-layout weights into the kernel layouts held in HBM.
+
+Input: any mapping from the reference's state-dict keys (modeling_siglip.py /
+modeling_gemma.py / modeling_paligemma.py module tree) to
+tensors of any float dtype on any device.  Output, on the HIP device:
+
+  SigLIP   patch W [hv][Kp] bf16 (Conv2d weight flattened (c, kh, kw), K padded to 64)
+           per layer: qkv W [3hv][hv] (query | key | value rows) + fp32 bias, out W, fc1 W
+           [Ip][hv] (N padded to 64, zero rows), fc2 W [hv][Ip] (K padded), fp32 LN params
+  proj     W [P][hv] bf16
+  Gemma    embed [V][H] bf16 (gather AND tied lm_head, modeling_gemma.py:492-499), lm_head bias fp32,
+           per layer: qkv W [(nh+2nkv)*hd][H] (q | k | v), o W, gate/up W [2I][H] interleaved in
+           16-row blocks (gate 16u..16u+15, then up 16u..16u+15) for the fused GELU*mul epilogue,
+           down W [H][I], fp32 RMSNorm weights (the kernel applies 1 + w).
+
+Padding rows/columns are zero so padded outputs are exactly 0 (gelu(0) = 0).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def _rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class PackedWeights:
+    def __init__(self, cfg: dict, get, device="cuda"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        v, t = cfg["vision_config"], cfg["text_config"]
+        dev = self.device
+
+        def bf(x):
+            return x.detach().to(device=dev, dtype=torch.bfloat16).contiguous()
+
+        def f32(x):
+            return x.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+        # ---------------- SigLIP
+        hv, iv = v["hidden_size"], v["intermediate_size"]
+        self.v_hidden, self.v_heads = hv, v["num_attention_heads"]
+        self.v_head_dim = hv // self.v_heads
+        self.v_layers = v["num_hidden_layers"]
+        self.v_eps = v.get("layer_norm_eps", 1e-6)
+        self.patch = v["patch_size"]
+        self.channels = v.get("num_channels", 3)
+        self.image_size = v.get("image_size", 224)
+        self.n_img = (self.image_size // self.patch) ** 2
+        pre = "vision_tower.model."
+        kraw = self.channels * self.patch * self.patch
+        self.patch_k = _rup(kraw, 64)
+        pw = torch.zeros(hv, self.patch_k, dtype=torch.bfloat16, device=dev)
+        pw[:, :kraw] = bf(get(pre + "embeddings.patch_embedding.weight").reshape(hv, kraw))
+        self.patch_w = pw
+        self.patch_b = f32(get(pre + "embeddings.patch_embedding.bias"))
+        self.pos_emb = f32(get(pre + "embeddings.positional_embeddings.weight"))
+        self.v_inter = _rup(iv, 64)
+        self.vl = []
+        for i in range(self.v_layers):
+            lp = f"{pre}encoder.layers.{i}."
+            a = lp + "self_attn."
+            qkv_w = torch.cat([bf(get(a + "query_proj.weight")), bf(get(a + "key_proj.weight")),
+                               bf(get(a + "value_proj.weight"))], 0).contiguous()
+            qkv_b = torch.cat([f32(get(a + "query_proj.bias")), f32(get(a + "key_proj.bias")),
+                               f32(get(a + "value_proj.bias"))], 0).contiguous()
+            fc1_w = torch.zeros(self.v_inter, hv, dtype=torch.bfloat16, device=dev)
+            fc1_w[:iv] = bf(get(lp + "mlp.fc1.weight"))
+            fc1_b = torch.zeros(self.v_inter, dtype=torch.float32, device=dev)
+            fc1_b[:iv] = f32(get(lp + "mlp.fc1.bias"))
+            fc2_w = torch.zeros(hv, self.v_inter, dtype=torch.bfloat16, device=dev)
+            fc2_w[:, :iv] = bf(get(lp + "mlp.fc2.weight"))
+            self.vl.append(dict(
+                ln1_w=f32(get(lp + "layer_norm1.weight")), ln1_b=f32(get(lp + "layer_norm1.bias")),
+                qkv_w=qkv_w, qkv_b=qkv_b,
+                o_w=bf(get(a + "out_proj.weight")), o_b=f32(get(a + "out_proj.bias")),
+                ln2_w=f32(get(lp + "layer_norm2.weight")), ln2_b=f32(get(lp + "layer_norm2.bias")),
+                fc1_w=fc1_w, fc1_b=fc1_b, fc2_w=fc2_w, fc2_b=f32(get(lp + "mlp.fc2.bias"))))
+        self.post_w = f32(get(pre + "post_layernorm.weight"))
+        self.post_b = f32(get(pre + "post_layernorm.bias"))
+        self.proj_w = bf(get("multi_modal_projector.linear.weight"))
+        self.proj_dim = self.proj_w.shape[0]
+
+        # ---------------- Gemma
+        self.hidden = t["hidden_size"]
+        self.heads = t["num_attention_heads"]
+        self.kv_heads = t["num_key_value_heads"]
+        self.head_dim = t.get("head_dim", 256)
+        self.inter = t["intermediate_size"]
+        self.t_layers = t["num_hidden_layers"]
+        self.vocab = t["vocab_size"]
+        self.rope_theta = t.get("rope_theta", 10000.0)
+        if self.inter % 16:
+            raise ValueError("intermediate_size must be a multiple of 16 for the gate/up interleave")
+        lm = "language_model."
+        self.embed = bf(get(lm + "model.embed_tokens.weight"))
+        self.lm_bias = f32(get(lm + "lm_head.bias"))
+        H, I = self.hidden, self.inter
+        self.tl = []
+        for i in range(self.t_layers):
+            lp = f"{lm}model.layers.{i}."
+            a = lp + "self_attn."
+            qkv_w = torch.cat([bf(get(a + "q_proj.weight")), bf(get(a + "k_proj.weight")),
+                               bf(get(a + "v_proj.weight"))], 0).contiguous()
+            g = bf(get(lp + "mlp.gate_proj.weight")).reshape(I // 16, 16, H)
+            u = bf(get(lp + "mlp.up_proj.weight")).reshape(I // 16, 16, H)
+            gu = torch.stack([g, u], dim=1).reshape(2 * I, H).contiguous()
+            self.tl.append(dict(
+                in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=qkv_w, o_w=bf(get(a + "o_proj.weight")),
+                post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=gu,
+                down_w=bf(get(lp + "mlp.down_proj.weight"))))
+            del g, u
+        self.final_w = f32(get(lm + "model.norm.weight"))
+        self.qkv_n = (self.heads + 2 * self.kv_heads) * self.head_dim
+
+    def nbytes(self) -> int:
+        n = 0
+        for k, x in vars(self).items():
+            if isinstance(x, torch.Tensor):
+                n += x.numel() * x.element_size()
+        for lst in (self.vl, self.tl):
+            for d in lst:
+                n += sum(x.numel() * x.element_size() for x in d.values())
+        return n
+
+    def decode_weight_bytes(self) -> int:
+        """HBM bytes of weights one decode step streams (Gemma linears + tied lm_head)."""
+        n = sum(sum(d[k].numel() * 2 for k in ("qkv_w", "o_w", "gu_w", "down_w")) for d in self.tl)
+        return n + self.embed.numel() * 2

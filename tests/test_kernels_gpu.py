@@ -1,0 +1,280 @@
+"""Per-kernel numerics on the HIP device: each libpghip entry point against a plain
+PyTorch fp32 reference of the same op on the same (bf16-representable) inputs."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    from pghip import _lib
+    _lib.load()
+
+
+def err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).cuda()
+
+
+def test_synth_fill_bit_identical_to_numpy():
+    from oracle import synth
+    from pghip import synthetic
+    for name, shape in [("language_model.model.layers.3.mlp.gate_proj.weight", (64, 2048)),
+                        ("vision_tower.model.encoder.layers.0.layer_norm1.weight", (1152,)),
+                        ("language_model.lm_head.bias", (4096,))]:
+        ref = synth.generate(name, shape)
+        g32 = synthetic.generate(name, shape, dtype=torch.float32).cpu().numpy()
+        g16 = synthetic.generate(name, shape, dtype=torch.bfloat16).float().cpu().numpy()
+        assert np.array_equal(ref.view(np.uint32), g32.view(np.uint32)), name
+        assert np.array_equal(ref, g16), name
+
+
+@pytest.mark.parametrize("M", [1, 3, 16, 17, 200, 300])
+@pytest.mark.parametrize("N,K", [(256, 128), (2560, 2048), (300, 192)])
+def test_gemm_plain_and_bias(M, N, K):
+    from pghip import ops
+    A, W = rnd(M, K, seed=1), rnd(N, K, scale=1 / math.sqrt(K), seed=2)
+    bias = torch.randn(N).cuda()
+    ref = A.float() @ W.float().t() + bias
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, W, out, bias=bias)
+    assert err(out, ref) < 1e-2
+    outf = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    ops.gemm(A, W, outf, epi=ops.EPI_F32, bias=bias)
+    assert err(outf, ref) < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 8, 64, 264])
+def test_gemm_split_k_partials(M):
+    from pghip import ops
+    K, N = 4096, 512
+    A, W = rnd(M, K, seed=3), rnd(N, K, scale=1 / 64, seed=4)
+    bias = torch.randn(N).cuda()
+    for s in (1, 2, 4):
+        part = torch.empty(s, M, N, dtype=torch.float32, device="cuda")
+        ops.gemm(A, W, part, epi=ops.EPI_F32, bias=bias, ksplit=s)
+        assert err(part.sum(0), A.float() @ W.float().t() + bias) < 1e-5
+
+
+@pytest.mark.parametrize("M", [1, 16, 150])
+def test_gemm_gelu_and_gelu_mul(M):
+    from pghip import ops
+    K, I = 256, 320
+    A = rnd(M, K, seed=5)
+    g, u = rnd(I, K, scale=0.1, seed=6), rnd(I, K, scale=0.1, seed=7)
+    gu = torch.stack([g.view(I // 16, 16, K), u.view(I // 16, 16, K)], 1).reshape(2 * I, K).contiguous()
+    out = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, gu, out, epi=ops.EPI_BF16_GELU_MUL)
+    ref = torch.nn.functional.gelu(A.float() @ g.float().t(), approximate="tanh") * (A.float() @ u.float().t())
+    assert err(out, ref) < 1e-2
+    bias = torch.randn(I).cuda() * 0.1
+    out2 = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, g, out2, epi=ops.EPI_BF16_GELU, bias=bias)
+    assert err(out2, torch.nn.functional.gelu(A.float() @ g.float().t() + bias, approximate="tanh")) < 1e-2
+
+
+def test_gemm_vt_and_pos_epilogues():
+    from pghip import ops
+    M, K, hv = 40, 192, 64
+    A, W = rnd(M, K, seed=8), rnd(3 * hv, K, scale=0.1, seed=9)
+    bias = torch.randn(3 * hv).cuda()
+    out = torch.zeros(M, 3 * hv, dtype=torch.bfloat16, device="cuda")
+    vt = torch.zeros(hv, M, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, W, out, epi=ops.EPI_BF16_VT, bias=bias, aux_out=vt, aux_ld=M, aux_n=2 * hv)
+    ref = A.float() @ W.float().t() + bias
+    assert err(out[:, :2 * hv], ref[:, :2 * hv]) < 1e-2
+    assert err(vt, ref[:, 2 * hv:].t()) < 1e-2
+    pos = torch.randn(8, 3 * hv).cuda()
+    o2 = torch.empty(M, 3 * hv, dtype=torch.float32, device="cuda")
+    ops.gemm(A, W, o2, epi=ops.EPI_F32_POS, bias=bias, aux=pos, aux_rows=8)
+    assert err(o2, ref + pos[torch.arange(M) % 8]) < 1e-5
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("H", [128, 1152, 2048])
+def test_norm_residual(mode, H):
+    from pghip import ops
+    M, S = 37, 3
+    resid = torch.randn(M, H).cuda()
+    part = torch.randn(S, M, H).cuda()
+    w, b = torch.randn(H).cuda() * 0.1 + (1 if mode == 0 else 0), torch.randn(H).cuda() * 0.1
+    x = resid + part.sum(0)
+    if mode == 0:
+        ref = torch.nn.functional.layer_norm(x, (H,), w, b, 1e-6)
+    else:
+        ref = x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)
+    out = torch.empty(M, H, dtype=torch.bfloat16, device="cuda")
+    of = torch.empty(M, H, dtype=torch.float32, device="cuda")
+    ops.norm_residual(resid, w, b=b if mode == 0 else None, mode=mode, partials=part, nsplit=S, out=out, out_f32=of)
+    assert err(resid, x) < 1e-6
+    assert err(of, ref) < 1e-5
+    assert err(out, ref) < 1e-2
+
+
+def _attn_ref(q, k, v, scale, mask=None):
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    if mask is not None:
+        s = s + mask
+    return torch.softmax(s, -1) @ v.float()
+
+
+@pytest.mark.parametrize("B,N,nh,hd", [(1, 256, 16, 72), (2, 16, 8, 24), (1, 100, 4, 64)])
+def test_attention_vision_layout(B, N, nh, hd):
+    """SigLIP: q/k from the fused QKV buffer, V^T from the transposed side buffer."""
+    from pghip import ops
+    hv = nh * hd
+    M = B * N
+    qkv = rnd(M, 3 * hv, seed=10)
+    vt = qkv[:, 2 * hv:].t().contiguous()
+    o = torch.empty(M, hv, dtype=torch.bfloat16, device="cuda")
+    ops.attention(qkv, 3 * hv, o, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * M, M,
+                  B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=hd ** -0.5)
+    x = qkv.view(B, N, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    ref = _attn_ref(x[0], x[1], x[2], hd ** -0.5).permute(0, 2, 1, 3).reshape(M, hv)
+    assert err(o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("B,L,nh,nkv,hd,masked", [(1, 264, 8, 1, 256, False), (2, 24, 4, 1, 32, True),
+                                                  (1, 70, 8, 2, 64, False)])
+def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
+    """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode."""
+    from pghip import ops
+    Smax = 320
+    kvd = nkv * hd
+    q = rnd(B * L, nh * hd, seed=11)
+    kc = torch.zeros(B, Smax, kvd, dtype=torch.bfloat16, device="cuda")
+    vtc = torch.zeros(B, kvd, Smax, dtype=torch.bfloat16, device="cuda")
+    kk, vv = rnd(B, L, kvd, seed=12), rnd(B, L, kvd, seed=13)
+    kc[:, :L] = kk
+    vtc[:, :, :L] = vv.transpose(1, 2)
+    mask = None
+    if masked:
+        mask = torch.triu(torch.full((L, L), -1e9), 1).expand(B, L, L).contiguous().cuda()
+    o = torch.empty(B * L, nh * hd, dtype=torch.bfloat16, device="cuda")
+    ops.attention(q, nh * hd, o, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
+                  B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, mask=mask,
+                  mask_bs=(L * L if masked else 0), mask_rs=(L if masked else 0))
+    qh = q.view(B, L, nh, hd).transpose(1, 2)
+    g = nh // nkv
+    kh = kk.view(B, L, nkv, hd).transpose(1, 2).repeat_interleave(g, 1)
+    vh = vv.view(B, L, nkv, hd).transpose(1, 2).repeat_interleave(g, 1)
+    ref = _attn_ref(qh, kh, vh, hd ** -0.5, None if mask is None else mask[:, None])
+    assert err(o, ref.transpose(1, 2).reshape(B * L, nh * hd)) < 2e-2
+    # decode: the last row's query against all L keys, split-KV + combine, Lkv from device memory
+    if masked:
+        return
+    qd = q.view(B, L, nh * hd)[:, -1].contiguous()
+    lkv = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
+    SK = 64
+    nsplit = ((Smax + SK - 1) // SK + 3) // 4 * 4
+    dt = (hd + 15) // 16 * 16
+    po = torch.empty(B * nkv * nsplit * 16 * dt, device="cuda")
+    pml = torch.empty(B * nkv * nsplit * 16 * 2, device="cuda")
+    od = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
+    ops.attention(qd, nh * hd, od, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
+                  B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=SK,
+                  nsplit=nsplit, part_o=po, part_ml=pml)
+    ops.attn_combine(po, pml, od, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+    assert err(od, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2
+
+
+def test_rope_kv_write_matches_reference_formula():
+    from oracle import paligemma_oracle as O
+    from pghip import engine, ops
+    B, L, nh, nkv, hd, Smax = 2, 5, 4, 1, 32, 64
+    qkv = rnd(B * L, (nh + 2 * nkv) * hd, seed=14)
+    q0 = qkv.clone()
+    pos = (torch.arange(L) + 1).repeat(B).to(torch.int32).cuda()
+    cos_t, sin_t = engine.rope_tables(hd, 128, 10000.0, "cuda")
+    kc = torch.zeros(B, Smax, nkv * hd, dtype=torch.bfloat16, device="cuda")
+    vtc = torch.zeros(B, nkv * hd, Smax, dtype=torch.bfloat16, device="cuda")
+    ops.rope_kv_write(qkv, pos, cos_t, sin_t, kc, vtc, T=B * L, L=L, Hq=nh, Hkv=nkv, D=hd, Smax=Smax, slot_base=3)
+    x = q0.float().cpu().numpy().reshape(B, L, nh + 2, hd)
+    cos, sin = O.rope_cos_sin(hd, pos.cpu().numpy().reshape(B, L))
+    qr, kr = O.apply_rotary_pos_emb(x[:, :, :nh].transpose(0, 2, 1, 3), x[:, :, nh:nh + 1].transpose(0, 2, 1, 3),
+                                    cos, sin)
+    assert err(qkv[:, :nh * hd].float(), torch.from_numpy(qr.transpose(0, 2, 1, 3).reshape(B * L, -1))) < 1e-2
+    assert err(kc[:, 3:3 + L].float(), torch.from_numpy(kr.transpose(0, 2, 1, 3).reshape(B, L, -1))) < 1e-2
+    assert torch.equal(vtc[:, :, 3:3 + L].transpose(1, 2), q0.view(B, L, -1)[:, :, (nh + 1) * hd:])
+
+
+def test_im2col_merge_rank():
+    from pghip import ops
+    B, C, H, p = 2, 3, 28, 14
+    px = torch.randn(B, C, H, H).cuda()
+    out = torch.empty(B * 4, 640, dtype=torch.bfloat16, device="cuda")
+    ops.patch_im2col(px, p, out)
+    ref = px.view(B, C, 2, p, 2, p).permute(0, 2, 4, 1, 3, 5).reshape(B * 4, C * p * p)
+    assert torch.equal(out[:, :588], ref.to(torch.bfloat16)) and out[:, 588:].abs().max().item() == 0
+    ids = torch.tensor([[9, 9, 2, 5, 0, 9], [9, 0, 9, 7, 9, 3]], dtype=torch.int64).cuda()
+    rank = torch.empty(12, dtype=torch.int32, device="cuda")
+    ops.image_rank(ids.view(-1), 9, rank)
+    flat = ids.view(-1).cpu()
+    assert rank.cpu().tolist() == [int((flat[:i] == 9).sum()) for i in range(12)]
+    emb = rnd(16, 64, seed=15)
+    feat = torch.randn(6, 64).cuda()
+    res = torch.empty(12, 64, device="cuda")
+    ops.embed_merge(ids.view(-1), rank, emb, feat, 6, res, image_id=9, pad_id=0, img_scale=0.125, normalizer=8.0)
+    for i, t in enumerate(flat.tolist()):
+        if t == 0:
+            want = torch.zeros(64)
+        elif t == 9:
+            want = feat[int((flat[:i] == 9).sum())].cpu() * 0.125 * 8.0
+        else:
+            want = emb[t].float().cpu() * 8.0
+        assert torch.allclose(res[i].cpu(), want), i
+
+
+def test_argmax_first_index_and_state_advance():
+    from pghip import ops
+    V = 257216
+    x = torch.randn(3, V).cuda()
+    x[1, 1000] = 50.0
+    x[1, 77] = 50.0
+    ids = torch.empty(3, dtype=torch.int64, device="cuda")
+    ws = torch.empty(3 * 64 * 2, device="cuda")
+    hist = torch.zeros(4, 3, dtype=torch.int64, device="cuda")
+    step = torch.tensor([2], dtype=torch.int32, device="cuda")
+    pos = torch.tensor([5, 6, 7], dtype=torch.int32, device="cuda")
+    kv = torch.tensor([9], dtype=torch.int32, device="cuda")
+    ops.argmax(x, ids, ws, hist=hist, step=step, pos=pos, kv_len=kv)
+    want = torch.argmax(x.cpu(), -1)
+    assert ids.cpu().tolist() == want.tolist() and ids[1].item() == 77
+    assert hist[2].cpu().tolist() == want.tolist()
+    assert step.item() == 3 and kv.item() == 10 and pos.cpu().tolist() == [6, 7, 8]
+
+
+def test_topp_matches_reference_filter(golden):
+    from oracle import paligemma_oracle as O
+    from pghip import ops
+    g = golden("topp")
+    for ci in range(4):
+        logits = torch.from_numpy(g[f"c{ci}_logits"]).cuda()
+        T, P = float(g[f"c{ci}_T"]), float(g[f"c{ci}_p"])
+        V = logits.shape[1]
+        u = torch.tensor([[0.0], [0.37], [0.999]], dtype=torch.float32).cuda()
+        probs = torch.empty(1, V, device="cuda")
+        ids = torch.empty(1, dtype=torch.int64, device="cuda")
+        step = torch.zeros(1, dtype=torch.int32, device="cuda")
+        for k in range(3):
+            ops.topp_sample(logits, ids, u, temperature=T, top_p=P, step=step, probs_out=probs)
+            want = O.sample_top_p(logits.cpu().numpy(), T, P, u[k].cpu().numpy())[0, 0]
+            got = ids.item()
+            pr = probs.cpu().numpy()[0]
+            kept = set(np.nonzero(pr)[0].tolist())
+            ref_kept = set(g[f"c{ci}_kept_ids"].tolist())
+            assert len(kept ^ ref_kept) <= 1, (ci, len(kept), len(ref_kept))
+            assert got in kept
+            if kept == ref_kept:
+                assert got == want, (ci, k, got, want)
