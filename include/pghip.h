@@ -31,8 +31,35 @@ enum {
                                GemmaMLP gate/up (gemma:212-217)                                  */
   PG_EPI_F32 = 3,           /* C f32 [ksplit][M][ldc] partial slabs (+bias on slab 0)          */
   PG_EPI_F32_POS = 4,       /* C f32 = acc + bias + aux[(m % aux_rows)*ldc + n]   patch+pos emb  */
-  PG_EPI_BF16_VT = 5        /* cols < aux_n -> C bf16; cols >= aux_n -> aux_out[(n-aux_n)*aux_ld + m] */
+  PG_EPI_BF16_VT = 5,       /* cols < aux_n -> C bf16; cols >= aux_n -> aux_out[(n-aux_n)*aux_ld + m] */
+  PG_EPI_QKV_ROPE = 6       /* fused q|k|v (rope-permuted W rows): RoPE(q) -> C, RoPE(k) -> K cache, v -> V^T
+                               cache (gemma.py:274-302 + KVCache.update :18-57); pg_gemm_fused only          */
 };
+
+/* Fused-operation arguments of pg_gemm_fused (M <= 16 for the prologues). */
+typedef struct PgFusedArgs {
+  int pro_mode;             /* 0: x = A ; 1: x = RMSNorm(resid_in + sum partials)*(1+norm_w) (gemma.py:172-181) ;
+                               2: x = merge of split-KV attention partials (pg_attn_combine folded in)      */
+  const float* resid_in;
+  float* resid_out;         /* written once: resid_in + sum partials (ping-pong residual stream; may be NULL) */
+  const float* partials;    /* [nsplit][M][K] */
+  int nsplit;
+  const float* norm_w;
+  float eps;
+  const float* part_o;      /* [B][Hkv][asplit][16][dtw] from pg_attention (split mode) */
+  const float* part_ml;     /* [B][Hkv][asplit][16][2] */
+  int asplit, head_dim, dtw, q_per_kv, kv_heads;
+  const float* cos_t;       /* [P][head_dim/2] */
+  const float* sin_t;
+  const int* pos;           /* rotary position per output row */
+  int rows_per_batch;       /* row m -> batch m / L, cache slot slot_base + *slot_dev + m % L */
+  const int* slot_dev;
+  int slot_base;
+  void* kc;                 /* bf16 [B][smax][kv_heads*head_dim] */
+  void* vtc;                /* bf16 [B][kv_heads*head_dim][smax] */
+  int smax;
+  int q_heads;
+} PgFusedArgs;
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
  * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0
@@ -40,6 +67,10 @@ enum {
 int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
             int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
             int aux_ld, int aux_n, hipStream_t stream);
+
+/* pg_gemm + fused prologue / RoPE-KV epilogue (decode layer in 5 launches). */
+int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
+                  int M, int N, int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream);
 
 /* resid[row] += sum_s partials[s][row]; y = LayerNorm (mode 0, w, b) | Gemma RMSNorm (mode 1, (1+w)).
  * siglip.py:199,203,210,218,310,319 ; gemma.py:157-182,395,412,470.  y -> out bf16 (ldo) and/or out_f32. */

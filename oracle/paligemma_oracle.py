@@ -31,6 +31,29 @@ import numpy as np
 
 F32 = np.float32
 
+# bf16-operand emulation (test aid): when on, every GEMM/attention operand is rounded to
+# bf16 where the HIP path feeds bf16 to the MFMAs (activations into linears, q/k/v, RoPE'd
+# q/k, softmax P).  It separates "bf16 precision" from "kernel bug" in the GPU tests.
+_BF16_OPERANDS = False
+
+
+class bf16_operands:
+    def __enter__(self):
+        global _BF16_OPERANDS
+        self._old, _BF16_OPERANDS = _BF16_OPERANDS, True
+
+    def __exit__(self, *a):
+        global _BF16_OPERANDS
+        _BF16_OPERANDS = self._old
+
+
+def q16(x: np.ndarray) -> np.ndarray:
+    if not _BF16_OPERANDS:
+        return x
+    u = np.ascontiguousarray(x, dtype=F32).view(np.uint32)
+    u = (u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) & np.uint32(0xFFFF0000)
+    return u.view(F32)
+
 
 # --------------------------------------------------------------------------- #
 # elementwise helpers
@@ -59,7 +82,7 @@ def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float) -> np.nd
 
 def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:
     """nn.Linear: x @ w.T + b."""
-    y = x @ w.T
+    y = q16(x) @ w.T
     if b is not None:
         y = y + b
     return y.astype(F32, copy=False)
@@ -94,12 +117,12 @@ def siglip_attention(W: dict, lp: str, vcfg: dict, x: np.ndarray) -> np.ndarray:
     k = linear(x, W[lp + "key_proj.weight"], W[lp + "key_proj.bias"])      # :71
     q = linear(x, W[lp + "query_proj.weight"], W[lp + "query_proj.bias"])  # :73
     v = linear(x, W[lp + "value_proj.weight"], W[lp + "value_proj.bias"])  # :75
-    k = k.reshape(B, N, nh, hd).transpose(0, 2, 1, 3)                 # :79-89
-    q = q.reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
-    v = v.reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
+    k = q16(k).reshape(B, N, nh, hd).transpose(0, 2, 1, 3)            # :79-89
+    q = q16(q).reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
+    v = q16(v).reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
     s = (q @ k.transpose(0, 1, 3, 2)) * scale                          # :96-100
     p = softmax_lastdim(s)                                              # :122
-    o = p @ v                                                           # :136
+    o = q16(p) @ v                                                      # :136
     o = o.transpose(0, 2, 1, 3).reshape(B, N, E)                        # :148-153
     return linear(o, W[lp + "out_proj.weight"], W[lp + "out_proj.bias"])   # :156
 
@@ -197,11 +220,12 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     k = linear(x, W[lp + "k_proj.weight"])                              # :274
     v = linear(x, W[lp + "v_proj.weight"])                              # :276
     q = linear(x, W[lp + "q_proj.weight"])                              # :278
-    k = k.reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)                  # :285-287
-    v = v.reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)
-    q = q.reshape(B, L, nh, hd).transpose(0, 2, 1, 3)
+    k = q16(k).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)             # :285-287
+    v = q16(v).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)
+    q = q16(q).reshape(B, L, nh, hd).transpose(0, 2, 1, 3)
     cos, sin = rope_cos_sin(hd, position_ids, tcfg.get("rope_theta", 10000.0))  # :293
     q, k = apply_rotary_pos_emb(q, k, cos, sin)                         # :295
+    q, k = q16(q), q16(k)
     if kv_cache is not None:                                            # :301-302
         k, v = kv_cache.update(k, v, layer_idx)
     g = nh // nkv                                                       # repeat_kv :185-196
@@ -212,7 +236,7 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     assert mask is not None, "Attention Mask needss to be provided"    # :325
     s = s + mask                                                        # :326
     p = softmax_lastdim(s)                                              # :329
-    o = p @ v                                                           # :339
+    o = q16(p) @ v                                                      # :339
     if o.shape != (B, nh, L, hd):                                       # :341-345
         raise ValueError("Size Mismatch")
     o = o.transpose(0, 2, 1, 3).reshape(B, L, -1)                       # :354-355

@@ -32,18 +32,21 @@ struct AttnArgs {
   float* part_ml;          // [B][Hkv][nsplit][16][2]
 };
 
-static __device__ __forceinline__ u32x4 ld16_or0(const bf16_t* p, bool ok) {
-  return ok ? *(const u32x4*)p : u32x4{0u, 0u, 0u, 0u};
+// Branch-free guarded loads: the address is always valid (callers clamp it), the value is
+// zeroed by selects.  Conditional loads compiled to branches and, for partial blocks, to
+// serialised per-element loads + vmcnt(0) waits (profiles/r01: decode attention 16 us -> fixed).
+static __device__ __forceinline__ u32x4 ld16_sel(const bf16_t* p, bool ok) {
+  const u32x4 v = *(const u32x4*)p;
+  return u32x4{ok ? v[0] : 0u, ok ? v[1] : 0u, ok ? v[2] : 0u, ok ? v[3] : 0u};
 }
 
-// 4 consecutive keys of one Vt row, zero beyond kend
+// 4 consecutive keys of one Vt row (row padded so key+3 stays inside), zero beyond kend / invalid d
 static __device__ __forceinline__ u32x2 ld_vt4(const bf16_t* row, int key, int kend, bool dok) {
-  if (!dok) return u32x2{0u, 0u};
-  if (key + 3 < kend) return *(const u32x2*)(row + key);
-  uint32_t e[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) e[j] = (key + j < kend) ? (uint32_t)row[key + j] : 0u;
-  return u32x2{e[0] | (e[1] << 16), e[2] | (e[3] << 16)};
+  const u32x2 v = *(const u32x2*)(row + key);
+  const int nv = dok ? kend - key : 0;   // number of valid keys among the 4
+  const uint32_t lo = nv >= 2 ? v[0] : (nv == 1 ? (v[0] & 0xFFFFu) : 0u);
+  const uint32_t hi = nv >= 4 ? v[1] : (nv == 3 ? (v[1] & 0xFFFFu) : 0u);
+  return u32x2{lo, hi};
 }
 
 template <int DP, int DT>
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int d0 = 32 * s + 8 * g;
-      qf[s] = __builtin_bit_cast(bf16x8, ld16_or0(qp + d0, rvalid && d0 < D));
+      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
     }
   }
   const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
@@ -96,20 +99,36 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const float LOG2E = 1.4426950408889634f;
 
   for (int kb = kbeg; kb < kend; kb += 32) {
-    // ---- S^T for keys kb..kb+15 (sA) and kb+16..kb+31 (sB)
-    f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+    // issue every load of the block first (K rows for S^T, V^T rows for P.V): one memory round trip
+    // K rows past kend are clamped to a valid row: their scores are masked to -inf below
+    const int ka = min(kb + c, kend - 1), kbk = min(kb + 16 + c, kend - 1);
+    u32x4 kfa[KS], kfb[KS];
     {
-      const int ka = kb + c, kbk = kb + 16 + c;
       const bf16_t* pa = kbase + (long)ka * a.k_rs;
       const bf16_t* pb = kbase + (long)kbk * a.k_rs;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int d0 = 32 * s + 8 * g;
-        bf16x8 fa = __builtin_bit_cast(bf16x8, ld16_or0(pa + d0, ka < kend && d0 < D));
-        bf16x8 fb = __builtin_bit_cast(bf16x8, ld16_or0(pb + d0, kbk < kend && d0 < D));
-        sA = mfma16(fa, qf[s], sA);
-        sB = mfma16(fb, qf[s], sB);
+        kfa[s] = ld16_sel(pa + (d0 < D ? d0 : 0), d0 < D);
+        kfb[s] = ld16_sel(pb + (d0 < D ? d0 : 0), d0 < D);
       }
+    }
+    u32x4 vf[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int d = 16 * t + c;
+      const bool dok = d < D;
+      const bf16_t* vrow = vbase + (long)(dok ? d : D - 1) * a.vt_ds;
+      const u32x2 v0 = ld_vt4(vrow, kb + 4 * g, kend, dok);
+      const u32x2 v1 = ld_vt4(vrow, kb + 16 + 4 * g, kend, dok);
+      vf[t] = u32x4{v0[0], v0[1], v1[0], v1[1]};
+    }
+    // ---- S^T for keys kb..kb+15 (sA) and kb+16..kb+31 (sB)
+    f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      sA = mfma16(__builtin_bit_cast(bf16x8, kfa[s]), qf[s], sA);
+      sB = mfma16(__builtin_bit_cast(bf16x8, kfb[s]), qf[s], sB);
     }
     // lane holds S[key = kb + 4g + j][q = c] (sA) and S[key = kb + 16 + 4g + j][q = c] (sB)
     float x[8];
@@ -118,8 +137,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       const int k0 = kb + 4 * g + j, k1 = kb + 16 + 4 * g + j;
       float v0 = sA[j] * a.scale_log2, v1 = sB[j] * a.scale_log2;
       if (mrow) {
-        if (k0 < kend) v0 += mrow[k0] * LOG2E;
-        if (k1 < kend) v1 += mrow[k1] * LOG2E;
+        v0 += mrow[min(k0, kend - 1)] * LOG2E;
+        v1 += mrow[min(k1, kend - 1)] * LOG2E;
       }
       x[j] = k0 < kend ? v0 : -INFINITY;
       x[4 + j] = k1 < kend ? v1 : -INFINITY;
@@ -148,15 +167,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     pw[3] = pack_bf2(x[6], x[7]);
     const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const int d = 16 * t + c;
-      const bool dok = d < D;
-      const bf16_t* vrow = vbase + (long)(dok ? d : 0) * a.vt_ds;
-      u32x2 v0 = ld_vt4(vrow, kb + 4 * g, kend, dok);
-      u32x2 v1 = ld_vt4(vrow, kb + 16 + 4 * g, kend, dok);
-      u32x4 vv{v0[0], v0[1], v1[0], v1[1]};
-      o[t] = mfma16(__builtin_bit_cast(bf16x8, vv), pf, o[t]);
-    }
+    for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, o[t]);
   }
 
   // lane holds O^T[d = 16t + 4g + j][q = c]
@@ -187,26 +198,44 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   }
 }
 
-// Merge the split partials: out[b][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s
+// Merge the split partials: out[b][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s.
+// One workgroup per (b, kv head, q row of the group), one thread per d.
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
                                                            const float* __restrict__ part_ml, int nsplit, int G,
                                                            int Hkv, int D, int DTW, bf16_t* __restrict__ o, long o_rs) {
-  const int bk = blockIdx.x;  // b * Hkv + kvh
+  const int row = blockIdx.x % G;
+  const int bk = blockIdx.x / G;  // b * Hkv + kvh
   const int b = bk / Hkv, kvh = bk % Hkv;
-  for (int idx = threadIdx.x; idx < G * D; idx += blockDim.x) {
-    const int row = idx / D, d = idx % D;
-    float M = -INFINITY;
-    for (int s = 0; s < nsplit; ++s) M = fmaxf(M, part_ml[(((long)bk * nsplit + s) * 16 + row) * 2]);
-    float num = 0.f, den = 0.f;
-    for (int s = 0; s < nsplit; ++s) {
-      const long base = ((long)bk * nsplit + s) * 16 + row;
-      const float ms = part_ml[base * 2];
-      if (ms == -INFINITY) continue;
-      const float f = exp2f(ms - M);
-      num += f * part_o[base * DTW + d];
-      den += f * part_ml[base * 2 + 1];
+  __shared__ float wsh[256];
+  __shared__ float inv_den;
+  // split weights 2^(m_s - M) (thread s), and the denominator
+  float ms = -INFINITY, ls = 0.f;
+  if ((int)threadIdx.x < nsplit) {
+    const long base = ((long)bk * nsplit + threadIdx.x) * 16 + row;
+    ms = part_ml[base * 2];
+    ls = part_ml[base * 2 + 1];
+  }
+  float M = wave_max(ms);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = M;
+  __syncthreads();
+  M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float wgt = (ms == -INFINITY) ? 0.f : exp2f(ms - M);
+  if ((int)threadIdx.x < nsplit) wsh[threadIdx.x] = wgt;
+  float den = wave_sum(wgt * ls);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = den;
+  __syncthreads();
+  if (threadIdx.x == 0) inv_den = 1.0f / (red[0] + red[1] + red[2] + red[3]);
+  __syncthreads();
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float num = 0.f;
+#pragma unroll 8
+    for (int s2 = 0; s2 < nsplit; ++s2) {
+      const float wv = wsh[s2];
+      if (wv != 0.f) num += wv * part_o[(((long)bk * nsplit + s2) * 16 + row) * DTW + d];
     }
-    o[(long)b * o_rs + (long)(kvh * G + row) * D + d] = f2bf(num / den);
+    o[(long)b * o_rs + (long)(kvh * G + row) * D + d] = f2bf(num * inv_den);
   }
 }
 
@@ -216,6 +245,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
     launched = true;                                                                         \
   }
 
+// V^T rows must be readable up to key 32*ceil(Lkv/32) (pad the row by 32 elements).
 // q/o row for (b, pos, head): q + (b*Lq + pos)*q_rs + head*D.  k for (b, key, kvh): k + b*k_bs + kvh*k_hs + key*k_rs.
 // vt for (b, d, key, kvh): vt + b*vt_bs + kvh*vt_hs + d*vt_ds + key.  mask (optional, additive fp32): mask + b*mask_bs
 // + pos*mask_rs + key.  Lkv = (lkv_dev ? *lkv_dev : 0) + Lkv.
@@ -256,9 +286,9 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
 
 extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                                void* o, long o_rs, hipStream_t stream) {
-  PG_REQUIRE(Hq % Hkv == 0 && Hq / Hkv <= 16);
+  PG_REQUIRE(Hq % Hkv == 0 && Hq / Hkv <= 16 && nsplit <= 256);
   const int DT = (D + 15) / 16;
-  hipLaunchKernelGGL(attn_combine_kernel, dim3(B * Hkv), dim3(256), 0, stream, part_o, part_ml, nsplit, Hq / Hkv,
+  hipLaunchKernelGGL(attn_combine_kernel, dim3(B * Hq), dim3(256), 0, stream, part_o, part_ml, nsplit, Hq / Hkv,
                      Hkv, D, DT * 16, (bf16_t*)o, o_rs);
   PG_LAUNCH_CHECK();
   return 0;

@@ -10,7 +10,7 @@
 //    (MFMA-A = W, MFMA-B = A) so each lane ends with 4 consecutive n of one m —
 //    8/16-byte epilogue stores.  Used for prefill (M = tokens).
 //  * gemv_kernel      : M <= 16 (decode).  Weight streaming: each wave reads
-//    16 rows of W with 16U-byte contiguous non-temporal loads per lane straight
+//    16 rows of W with 16U-byte contiguous loads per lane straight
 //    into VGPRs (no LDS round trip), the k order inside an MFMA step is permuted
 //    identically for both operands so a lane's bytes are contiguous; 4 waves per
 //    workgroup split K and reduce through LDS; an optional second level of
@@ -27,6 +27,35 @@ enum {
   PG_EPI_F32 = 3,           // C f32 [z][M][ldc] = acc (+ bias on split 0)
   PG_EPI_F32_POS = 4,       // C f32 = acc + bias + aux[(m % aux_rows) * ldc + n]  (patch + position emb)
   PG_EPI_BF16_VT = 5,       // n < aux_n: C bf16 = acc + bias ; n >= aux_n: aux_out bf16 [(n-aux_n)][m] (ld aux_ld)
+  PG_EPI_QKV_ROPE = 6,      // fused q|k|v projection (rope-permuted W rows): RoPE on q -> C, RoPE on k -> K cache,
+                            // v -> V^T cache (GemmaAttention.forward :274-302 + KVCache.update)
+};
+
+// Extra arguments of the fused entry point pg_gemm_fused (mirrors PgFusedArgs in include/pghip.h).
+struct PgFusedArgs {
+  // prologue: 0 = x read from A (bf16), 1 = x = RMSNorm(resid_in + sum partials) * (1 + norm_w),
+  //           2 = x = merge of split-KV attention partials (pg_attn_combine folded into the GEMV)
+  int pro_mode;
+  const float* resid_in;
+  float* resid_out;          // written once (workgroup 0) with resid_in + sum partials (may be null)
+  const float* partials;     // [nsplit][M][K]
+  int nsplit;
+  const float* norm_w;
+  float eps;
+  const float* part_o;       // attention partials [B][Hkv][asplit][16][dtw]
+  const float* part_ml;      // [B][Hkv][asplit][16][2]
+  int asplit, head_dim, dtw, q_per_kv, kv_heads;
+  // RoPE / KV-cache epilogue (PG_EPI_QKV_ROPE)
+  const float* cos_t;
+  const float* sin_t;
+  const int* pos;            // rotary position per output row m
+  int rows_per_batch;        // L (row m -> batch m / L, in-batch index m % L)
+  const int* slot_dev;       // cache slot base from device memory (may be null)
+  int slot_base;
+  bf16_t* kc;                // [B][Smax][Hkv*D]
+  bf16_t* vtc;               // [B][Hkv*D][Smax]
+  int smax;
+  int q_heads;
 };
 
 struct EpiArgs {
@@ -39,7 +68,52 @@ struct EpiArgs {
   bf16_t* aux_out;
   int aux_ld;
   int aux_n;
+  PgFusedArgs f;
 };
+
+// RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are
+// packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
+// the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).
+__device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
+  f32x4 pr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+  if (m >= e.M || n0 >= e.N) return;
+  const PgFusedArgs& f = e.f;
+  const int D = f.head_dim, half = D >> 1;
+  const int blk = n0 / D, within = n0 % D;
+  const int t = within >> 4, jj0 = within & 15;
+  const bool second = jj0 >= 8;
+  const int ii = 8 * t + (jj0 & 7);                   // index in [0, D/2) of element 0
+  const int d0 = second ? half + ii : ii;             // original dim of element 0
+  const int b = m / f.rows_per_batch, i = m % f.rows_per_batch;
+  const int slot = f.slot_base + (f.slot_dev ? *f.slot_dev : 0) + i;
+  const int Hq = f.q_heads, Hkv = f.kv_heads;
+  const int KV = Hkv * D;
+  if (blk < Hq + Hkv) {
+    const int p = f.pos[m];
+    const float* cs = f.cos_t + (long)p * half + ii;
+    const float* sn = f.sin_t + (long)p * half + ii;
+    f32x4 y;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // q*cos + rotate_half(q)*sin, rotate_half(x) = cat(-x2, x1)  (modeling_gemma.py:138-151)
+      y[j] = second ? v[j] * cs[j] + pr[j] * sn[j] : v[j] * cs[j] - pr[j] * sn[j];
+    }
+    u32x2 pk;
+    pk[0] = pack_bf2(y[0], y[1]);
+    pk[1] = pack_bf2(y[2], y[3]);
+    if (blk < Hq) {
+      *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0) = pk;
+    } else {
+      *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
+    }
+  } else {
+    const int c0 = (blk - Hq - Hkv) * D + d0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
+  }
+}
 
 // Store 4 consecutive columns n0..n0+3 of row m (values v).  z = split index.
 template <int EPI>
@@ -213,6 +287,9 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
 #pragma unroll
       for (int j = 0; j < 4; j += 2) epi_gelu_mul4(e, m, n0 + wn * 64 + j * 16, q, acc[i][j], acc[i][j + 1]);
+    } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) epi_qkv_rope4(e, m, n0 + wn * 64 + j * 16 + q, acc[i][j]);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) epi_store4<EPI>(e, m, n0 + wn * 64 + j * 16 + q, acc[i][j], z);
@@ -223,39 +300,154 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 // --------------------------------------------------------------------------------------
 // Skinny GEMM / GEMV (M <= 16): weight streaming straight to VGPRs
 // --------------------------------------------------------------------------------------
-// One workgroup = 4 waves = NT adjacent 16-row tiles of W (NT = 2 for the interleaved
-// gate/up pair) over the K range of split blockIdx.y; the 4 waves split that range.
-// lane (r = lane&15, g = lane>>4) covers k = kc + 8U*g + [0, 8U): MFMA step s uses k = kc + 8U*g + 8s + [0,8)
-// for both operands (same permutation of k on both sides leaves the dot product unchanged).
-template <int U>
-__device__ __forceinline__ void gemv_w_load(const bf16_t* __restrict__ wrow, int kc, int g, u32x4* wv) {
-  const int off = kc + g * 8 * U;
+// One workgroup = 4 waves on NT adjacent 16-row tiles of W (NT = 2 for the interleaved gate/up
+// pair); the 4 waves split the chunks of split blockIdx.y round-robin and reduce through LDS.
+// Chunk = 32U k: lane (r = lane&15, g = lane>>4) loads 16U contiguous bytes of W row r at
+// k = chunk + 8U*g; MFMA step s consumes k = chunk + 8U*g + 8s + [0,8) for BOTH operands, a
+// permutation of k that leaves the dot product unchanged.  DEPTH chunks stay in flight in a
+// statically indexed register ring.  Plain (temporal) loads: measured 1.2-1.6x faster than
+// non-temporal ones on every decode shape (scripts/tune/tune_gemv.py).
+//
+// PRO (prologue, fuses the producer of x into the GEMV so a decode layer needs 5 launches):
+//   0: x rows read from A (bf16)
+//   1: x = RMSNorm(resid_in + sum_s partials[s]) * (1 + w)       (GemmaRMSNorm, modeling_gemma.py:172-181)
+//      workgroup (0,0) also writes resid_out = resid_in + sum partials (ping-pong residual stream)
+//   2: x = merge of the split-KV attention partials (2^(m_s - M) weighted, / sum l)
+// For PRO != 0 the WG's K range of x is built in LDS (bf16, rows padded by 16 B against bank conflicts).
+#define XPAD 8
+
+template <int PRO>
+__device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, int k0, int Kr, bf16_t* xs,
+                                              float* scratch) {
+  const PgFusedArgs& f = e.f;
+  const int t = threadIdx.x;
+  const int ldx = Kr + XPAD;
+  if constexpr (PRO == 1) {
+    // RMSNorm over the FULL row (Kr == K): pass 1 sum of squares, pass 2 normalise into LDS
+    const int K4 = K >> 2;
+    const bool w0 = blockIdx.x == 0 && blockIdx.y == 0 && f.resid_out != nullptr;
+    float* red = scratch;   // [4 waves][16 rows]
+    if (M == 1 && K4 <= 4 * 256) {
+      // one row: keep it in registers between the two passes (one dependent round trip fewer)
+      f32x4 v[4];
+      float ss = 0.f;
 #pragma unroll
-  for (int s = 0; s < U; ++s) wv[s] = __builtin_nontemporal_load((const u32x4*)(wrow + off + 8 * s));
-}
-template <int U>
-__device__ __forceinline__ void gemv_x_load(const bf16_t* __restrict__ xrow, bool xvalid, int kc, int g, u32x4* xv) {
-  const int off = kc + g * 8 * U;
+      for (int i = 0; i < 4; ++i) {
+        const int c = t + i * 256;
+        v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (c < K4) {
+          f32x4 a = ((const f32x4*)f.resid_in)[c];
+          for (int sp = 0; sp < f.nsplit; ++sp) a += ((const f32x4*)(f.partials + (size_t)sp * K))[c];
+          v[i] = a;
+          ss += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
+          if (w0) ((f32x4*)f.resid_out)[c] = a;
+        }
+      }
+      ss = wave_sum(ss);
+      if ((t & 63) == 0) red[t >> 6] = ss;
+      __syncthreads();
+      const float rstd = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + f.eps);
 #pragma unroll
-  for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xrow + off + 8 * s) : u32x4{0u, 0u, 0u, 0u};
+      for (int i = 0; i < 4; ++i) {
+        const int c = t + i * 256;
+        if (c < K4) {
+          const f32x4 w = ((const f32x4*)f.norm_w)[c];
+          u32x2 pk;
+          pk[0] = pack_bf2((v[i][0] * rstd) * (1.0f + w[0]), (v[i][1] * rstd) * (1.0f + w[1]));
+          pk[1] = pack_bf2((v[i][2] * rstd) * (1.0f + w[2]), (v[i][3] * rstd) * (1.0f + w[3]));
+          *(u32x2*)(xs + c * 4) = pk;
+        }
+      }
+      __syncthreads();
+      return;
+    }
+    for (int m = 0; m < M; ++m) {
+      float ss = 0.f;
+      for (int c = t; c < K4; c += 256) {
+        f32x4 v = ((const f32x4*)(f.resid_in + (size_t)m * K))[c];
+        for (int sp = 0; sp < f.nsplit; ++sp) v += ((const f32x4*)(f.partials + ((size_t)sp * M + m) * K))[c];
+        ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+        if (w0) ((f32x4*)(f.resid_out + (size_t)m * K))[c] = v;
+      }
+      ss = wave_sum(ss);
+      if ((t & 63) == 0) red[(t >> 6) * 16 + m] = ss;
+    }
+    __syncthreads();
+    for (int m = 0; m < M; ++m) {
+      const float rstd = rsqrtf((red[m] + red[16 + m] + red[32 + m] + red[48 + m]) / (float)K + f.eps);
+      for (int c = t; c < K4; c += 256) {
+        f32x4 v = ((const f32x4*)(f.resid_in + (size_t)m * K))[c];
+        for (int sp = 0; sp < f.nsplit; ++sp) v += ((const f32x4*)(f.partials + ((size_t)sp * M + m) * K))[c];
+        const f32x4 w = ((const f32x4*)f.norm_w)[c];
+        u32x2 pk;
+        pk[0] = pack_bf2((v[0] * rstd) * (1.0f + w[0]), (v[1] * rstd) * (1.0f + w[1]));
+        pk[1] = pack_bf2((v[2] * rstd) * (1.0f + w[2]), (v[3] * rstd) * (1.0f + w[3]));
+        *(u32x2*)(xs + m * ldx + c * 4) = pk;
+      }
+    }
+  } else if constexpr (PRO == 2) {
+    // x[m][k], k = hq*D + d over this WG's K range; partial row of q head hq: (kvh = hq / G, row = hq % G)
+    const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
+    const int h0 = k0 / D, nh = Kr / D;
+    float* wsc = scratch;              // [M*nh][S] weights, then [M*nh] 1/den at the end
+    const int pairs = M * nh;
+    for (int idx = t; idx < pairs * S; idx += 256) {
+      const int pr = idx / S, sp = idx % S;
+      const int m = pr / nh, hq = h0 + pr % nh;
+      const long base = (((long)m * f.kv_heads + hq / G) * S + sp) * 16 + (hq % G);
+      wsc[idx] = f.part_ml[base * 2];
+    }
+    __syncthreads();
+    float* inv = scratch + pairs * S;
+    for (int pr = t; pr < pairs; pr += 256) {
+      const int m = pr / nh, hq = h0 + pr % nh;
+      float Mx = -INFINITY;
+      for (int sp = 0; sp < S; ++sp) Mx = fmaxf(Mx, wsc[pr * S + sp]);
+      float den = 0.f;
+      for (int sp = 0; sp < S; ++sp) {
+        const float ms = wsc[pr * S + sp];
+        const float w = ms == -INFINITY ? 0.f : exp2f(ms - Mx);
+        const long base = (((long)m * f.kv_heads + hq / G) * S + sp) * 16 + (hq % G);
+        den += w * f.part_ml[base * 2 + 1];
+        wsc[pr * S + sp] = w;
+      }
+      inv[pr] = 1.0f / den;
+    }
+    __syncthreads();
+    for (int idx = t; idx < M * Kr; idx += 256) {
+      const int m = idx / Kr, kk = idx % Kr;
+      const int hl = kk / D, d = kk % D, hq = h0 + hl;
+      const int pr = m * nh + hl;
+      const long base0 = (((long)m * f.kv_heads + hq / G) * S) * 16 + (hq % G);
+      float num = 0.f;
+#pragma unroll 8
+      for (int sp = 0; sp < S; ++sp) num += wsc[pr * S + sp] * f.part_o[(base0 + (long)sp * 16) * f.dtw + d];
+      xs[m * ldx + kk] = f2bf(num * inv[pr]);
+    }
+  }
+  __syncthreads();
 }
 
-template <int EPI, int NT>
+template <int EPI, int NT, int U, int DEPTH, int PRO>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
-                                                   const bf16_t* __restrict__ W, int ldw, int K, int kchunk, EpiArgs e) {
-  constexpr int U = 4;                       // MFMA steps per contiguous chunk (U*32 k, 16U bytes per lane)
+                                                   const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
+  constexpr int CH = U * 32;
+  extern __shared__ __attribute__((aligned(16))) char dyn_smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int r = lane & 15;
-  const int tile0 = blockIdx.x * NT;         // first 16-row tile of W
-  const int z = blockIdx.y;
-  const int kbeg = z * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  const int tile0 = blockIdx.x * NT;
   const int M = e.M;
-
   const bool xvalid = r < M;
-  const bf16_t* xrow = A + (size_t)(xvalid ? r : 0) * lda;
+
+  const int z = blockIdx.y;
+  const int nch_all = K / CH;
+  const int per_z = (nch_all + gridDim.y - 1) / gridDim.y;
+  const int c0 = z * per_z;
+  const int nch = min(nch_all - c0, per_z);
+  const int mine = nch > wave ? (nch - wave + 3) / 4 : 0;   // chunks wave, wave+4, ...
+
   const bf16_t* wrow[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -263,75 +455,81 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     n = n < e.N ? n : e.N - 1;
     wrow[t] = W + (size_t)n * ldw;
   }
-
   f32x4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // big chunks of U*32 k, round-robin over the 4 waves, software-pipelined by one chunk
-  const int CH = U * 32;
-  const int nbig = (kend - kbeg) / CH;
-  int c = wave;
-  if (c < nbig) {
-    u32x4 wv[NT][U], xv[U];
+  bf16_t* xs = (bf16_t*)dyn_smem;
+  const int Kr = per_z * CH;                    // K range of this split (LDS row length)
+  const bf16_t* xrow = PRO == 0 ? A + (size_t)(xvalid ? r : 0) * lda : nullptr;
+  const bf16_t* xlds = xs + (xvalid ? r : 0) * (Kr + XPAD);
+
+  u32x4 wb[DEPTH][NT][U];
+  u32x4 xb[DEPTH][U];
+  auto loadw = [&](int j, u32x4 (&wv)[NT][U]) {
+    const int off = (c0 + wave + j * 4) * CH + g * 8 * U;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) gemv_w_load<U>(wrow[t], kbeg + c * CH, g, wv[t]);
-    gemv_x_load<U>(xrow, xvalid, kbeg + c * CH, g, xv);
-    while (true) {
-      const int cn = c + 4;
-      u32x4 wn[NT][U], xn[U];
-      if (cn < nbig) {
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int t = 0; t < NT; ++t) gemv_w_load<U>(wrow[t], kbeg + cn * CH, g, wn[t]);
-        gemv_x_load<U>(xrow, xvalid, kbeg + cn * CH, g, xn);
+      for (int s = 0; s < U; ++s) wv[t][s] = *(const u32x4*)(wrow[t] + off + 8 * s);
+  };
+  auto loadx = [&](int j, u32x4 (&xv)[U]) {
+    const int koff = (wave + j * 4) * CH + g * 8 * U;     // offset inside this split
+    if constexpr (PRO == 0) {
+#pragma unroll
+      for (int s = 0; s < U; ++s)
+        xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
+    } else {
+#pragma unroll
+      for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  // (issuing the first weight chunks before the prologue measured no gain: the prologue's in-order
+  //  vmcnt waits drain them anyway)
+  if constexpr (PRO != 0) {
+    float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
+    gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch);
+  }
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (d < mine) {
+      loadw(d, wb[d]);
+      loadx(d, xb[d]);
+    }
+  for (int base = 0; base < mine; base += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      const int j = base + d;
+      if (j < mine) {
+#pragma unroll
+        for (int s = 0; s < U; ++s) {
+          const bf16x8 xv = __builtin_bit_cast(bf16x8, xb[d][s]);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wb[d][t][s]), xv, acc[t]);
+        }
+        if (j + DEPTH < mine) {
+          loadw(j + DEPTH, wb[d]);
+          loadx(j + DEPTH, xb[d]);
+        }
       }
-#pragma unroll
-      for (int s = 0; s < U; ++s) {
-        bf16x8 xb = __builtin_bit_cast(bf16x8, xv[s]);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wv[t][s]), xb, acc[t]);
-      }
-      if (cn >= nbig) break;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int s = 0; s < U; ++s) wv[t][s] = wn[t][s];
-#pragma unroll
-      for (int s = 0; s < U; ++s) xv[s] = xn[s];
-      c = cn;
     }
   }
-  // tail: single MFMA steps (32 k) round-robin
-  const int tbeg = kbeg + nbig * CH;
-  const int ntail = (kend - tbeg) / 32;
-  for (int ct = wave; ct < ntail; ct += 4) {
-    u32x4 wv[NT][1], xv[1];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) gemv_w_load<1>(wrow[t], tbeg + ct * 32, g, wv[t]);
-    gemv_x_load<1>(xrow, xvalid, tbeg + ct * 32, g, xv);
-    bf16x8 xb = __builtin_bit_cast(bf16x8, xv[0]);
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wv[t][0]), xb, acc[t]);
-  }
 
-  // reduce the 4 waves through LDS
   __shared__ f32x4 red[4][NT][64];
 #pragma unroll
   for (int t = 0; t < NT; ++t) red[wave][t][lane] = acc[t];
   __syncthreads();
   if (wave != 0) return;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    f32x4 s = red[0][t][lane];
-#pragma unroll
-    for (int w = 1; w < 4; ++w) s += red[w][t][lane];
-    acc[t] = s;
-  }
+  for (int t = 0; t < NT; ++t) acc[t] = red[0][t][lane] + red[1][t][lane] + red[2][t][lane] + red[3][t][lane];
   // lane holds C[m = lane&15][n = tile*16 + 4*(lane>>4) + 0..3]
   const int m = r;
   const int q = 4 * g;
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
     epi_gelu_mul4(e, m, tile0 * 16, q, acc[0], acc[1]);
+  } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) epi_qkv_rope4(e, m, (tile0 + t) * 16 + q, acc[t]);
   } else {
 #pragma unroll
     for (int t = 0; t < NT; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t], z);
@@ -350,21 +548,59 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   hipLaunchKernelGGL(gemm_tile_kernel<EPI>, grid, dim3(256), 0, st, A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
 }
 
-template <int EPI, int NT>
-static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
-                        hipStream_t st) {
+// measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
+// M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
+template <int EPI, int PRO>
+static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
+                            hipStream_t st) {
   const int ntiles = (e.N + 15) / 16;
-  int kchunk = ((K / 32 + ksplit - 1) / ksplit) * 32;
-  dim3 grid(ntiles / NT, ksplit);
-  hipLaunchKernelGGL((gemv_kernel<EPI, NT>), grid, dim3(256), 0, st, A, lda, W, ldw, K, kchunk, e);
+  const int CH = 64;                                   // U = 2
+  const int per_z = (K / CH + ksplit - 1) / ksplit;
+  size_t lds = 0;
+  if (PRO != 0) {
+    lds = (size_t)e.M * (per_z * CH + XPAD) * 2;
+    lds = (lds + 15) & ~(size_t)15;
+    if (PRO == 1) lds += 64 * sizeof(float);
+    if (PRO == 2) {
+      const int pairs = e.M * (per_z * CH / e.f.head_dim);
+      lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
+    }
+  }
+  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
+    dim3 grid((ntiles + 1) / 2, ksplit);
+    hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, 4, PRO>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
+  } else {
+    dim3 grid(ntiles, ksplit);
+    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, 8, PRO>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
+  }
 }
 
-extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
-                       int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
-                       int aux_ld, int aux_n, hipStream_t stream) {
+template <int EPI>
+static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
+                        hipStream_t st) {
+  switch (e.f.pro_mode) {
+    case 1: launch_gemv_pro<EPI, 1>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 2: launch_gemv_pro<EPI, 2>(A, lda, W, ldw, K, ksplit, e, st); break;
+    default: launch_gemv_pro<EPI, 0>(A, lda, W, ldw, K, ksplit, e, st); break;
+  }
+}
+
+static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
+                     int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
+                     int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
-  PG_REQUIRE(K % 32 == 0 && lda >= K && ldw >= K && (N % 4) == 0);
-  EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n};
+  PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
+  PgFusedArgs f{};
+  if (fa) f = *fa;
+  EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
+  if (f.pro_mode == 0) PG_REQUIRE(A != nullptr && lda >= K);
+  if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
+  if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
+  if (f.pro_mode == 2) PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 &&
+                                  f.asplit > 0 && f.q_per_kv > 0 && f.kv_heads > 0);
+  if (epi == PG_EPI_QKV_ROPE) PG_REQUIRE(f.head_dim % 16 == 0 && f.cos_t && f.sin_t && f.pos && f.kc && f.vtc &&
+                                         f.rows_per_batch > 0 && f.smax > 0 && ksplit == 1 &&
+                                         N == (f.q_heads + 2 * f.kv_heads) * f.head_dim);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
@@ -372,18 +608,19 @@ extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const flo
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
   if (M <= 16) {
-    PG_REQUIRE(N % 16 == 0 || epi == PG_EPI_F32 || epi == PG_EPI_BF16);
+    PG_REQUIRE(K % 64 == 0);
     switch (epi) {
-      case PG_EPI_BF16: launch_gemv<PG_EPI_BF16, 1>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU: launch_gemv<PG_EPI_BF16_GELU, 1>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU_MUL: launch_gemv<PG_EPI_BF16_GELU_MUL, 2>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32: launch_gemv<PG_EPI_F32, 1>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32_POS: launch_gemv<PG_EPI_F32_POS, 1>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_VT: launch_gemv<PG_EPI_BF16_VT, 1>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_BF16: launch_gemv<PG_EPI_BF16>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_BF16_GELU: launch_gemv<PG_EPI_BF16_GELU>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_BF16_GELU_MUL: launch_gemv<PG_EPI_BF16_GELU_MUL>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_F32: launch_gemv<PG_EPI_F32>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_F32_POS: launch_gemv<PG_EPI_F32_POS>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_BF16_VT: launch_gemv<PG_EPI_BF16_VT>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_QKV_ROPE: launch_gemv<PG_EPI_QKV_ROPE>(a, lda, w, ldw, K, ksplit, e, stream); break;
       default: return (int)hipErrorInvalidValue;
     }
   } else {
-    PG_REQUIRE(K % TBK == 0);
+    PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0);
     switch (epi) {
       case PG_EPI_BF16: launch_tile<PG_EPI_BF16>(a, lda, w, ldw, K, ksplit, e, stream); break;
       case PG_EPI_BF16_GELU: launch_tile<PG_EPI_BF16_GELU>(a, lda, w, ldw, K, ksplit, e, stream); break;
@@ -391,9 +628,22 @@ extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const flo
       case PG_EPI_F32: launch_tile<PG_EPI_F32>(a, lda, w, ldw, K, ksplit, e, stream); break;
       case PG_EPI_F32_POS: launch_tile<PG_EPI_F32_POS>(a, lda, w, ldw, K, ksplit, e, stream); break;
       case PG_EPI_BF16_VT: launch_tile<PG_EPI_BF16_VT>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_QKV_ROPE: launch_tile<PG_EPI_QKV_ROPE>(a, lda, w, ldw, K, ksplit, e, stream); break;
       default: return (int)hipErrorInvalidValue;
     }
   }
   PG_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
+                       int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
+                       int aux_ld, int aux_n, hipStream_t stream) {
+  return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, aux, aux_rows, aux_out, aux_ld, aux_n,
+                   nullptr, stream);
+}
+
+extern "C" int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
+                             int M, int N, int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream) {
+  return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream);
 }

@@ -14,10 +14,22 @@ LIB_PATH = os.path.join(_HERE, "libpghip.so")
 
 vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 
+class PgFusedArgs(C.Structure):
+    """Mirror of PgFusedArgs (include/pghip.h)."""
+    _fields_ = [("pro_mode", C.c_int), ("resid_in", C.c_void_p), ("resid_out", C.c_void_p),
+                ("partials", C.c_void_p), ("nsplit", C.c_int), ("norm_w", C.c_void_p), ("eps", C.c_float),
+                ("part_o", C.c_void_p), ("part_ml", C.c_void_p), ("asplit", C.c_int), ("head_dim", C.c_int),
+                ("dtw", C.c_int), ("q_per_kv", C.c_int), ("kv_heads", C.c_int), ("cos_t", C.c_void_p),
+                ("sin_t", C.c_void_p), ("pos", C.c_void_p), ("rows_per_batch", C.c_int), ("slot_dev", C.c_void_p),
+                ("slot_base", C.c_int), ("kc", C.c_void_p), ("vtc", C.c_void_p), ("smax", C.c_int),
+                ("q_heads", C.c_int)]
+
+
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
 SIGNATURES = {
     "pg_abi_version": [],
     "pg_gemm": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp],
+    "pg_gemm_fused": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
                      i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, vp],

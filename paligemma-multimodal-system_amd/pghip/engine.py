@@ -57,7 +57,7 @@ class KVStore:
 class PaliGemmaEngine:
     DECODE_SPLIT_O = 2      # split-K of o_proj at decode (partials reduced by the next RMSNorm)
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
-    DECODE_SPLIT_KEYS = 64  # keys per wave in split-KV decode attention
+    DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda"):
         self.cfg = cfg
@@ -93,7 +93,7 @@ class PaliGemmaEngine:
         return KVStore(w.t_layers, B, _rup(Smax, 64), w.kv_heads * w.head_dim, self.device)
 
     # ------------------------------------------------------------------ vision tower
-    def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False):
+    def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False, taps: Optional[list] = None):
         """SiglipVisionModel.forward + projector (modeling_siglip.py:312-334, modeling_paligemma.py:60-65).
         Returns image features fp32 [B*N][P] (projector output, unscaled) and optionally the
         post-LN vision output fp32 [B*N][hv]."""
@@ -106,9 +106,11 @@ class PaliGemmaEngine:
         ops.patch_im2col(px, w.patch, patches)
         resid = self._buf("v_resid", (M, hv), torch.float32)
         ops.gemm(patches, w.patch_w, resid, epi=ops.EPI_F32_POS, bias=w.patch_b, aux=w.pos_emb, aux_rows=N)
+        if taps is not None:
+            taps.append(resid.clone())
         xn = self._buf("v_xn", (M, hv), torch.bfloat16)
         qkv = self._buf("v_qkv", (M, 3 * hv), torch.bfloat16)
-        vt = self._buf("v_vt", (hv, M), torch.bfloat16)
+        vt = self._buf("v_vt", (hv, M + 32), torch.bfloat16)            # rows padded: attention reads 32-key blocks
         attn = self._buf("v_attn", (M, hv), torch.bfloat16)
         h = self._buf("v_h", (M, w.v_inter), torch.bfloat16)
         tiles = lambda n: ((M + 127) // 128) * ((n + 127) // 128)  # noqa: E731
@@ -119,8 +121,9 @@ class PaliGemmaEngine:
         for L in w.vl:
             ops.norm_residual(resid, L["ln1_w"], b=L["ln1_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
                               nsplit=ns, out=xn)
-            ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M, aux_n=2 * hv)
-            ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * M, M,
+            ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M + 32,
+                     aux_n=2 * hv)
+            ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
                           B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5))
             ops.gemm(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
             ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
@@ -128,6 +131,8 @@ class PaliGemmaEngine:
             ops.gemm(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"])
             ops.gemm(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
             ns = s_2
+            if taps is not None:                                          # debug: residual after the layer
+                taps.append((resid + part[:ns].sum(0)).clone())
         hid = torch.empty(M, hv, dtype=torch.float32, device=self.device) if want_hidden else None
         ops.norm_residual(resid, w.post_w, b=w.post_b, mode=ops.NORM_LAYER, eps=w.v_eps, partials=part, nsplit=ns,
                           out=xn, out_f32=hid)
@@ -149,7 +154,7 @@ class PaliGemmaEngine:
 
     def gemma_prefill(self, x_resid: torch.Tensor, positions: torch.Tensor, cache: KVStore, B: int, L: int,
                       logits_rows: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
-                      want_hidden: bool = False, want_logits: bool = True):
+                      want_hidden: bool = False, want_logits: bool = True, taps: Optional[list] = None):
         """GemmaForCausalLM.forward after the *sqrt(H) (modeling_gemma.py:510-534) on resid fp32 [B*L][H]
         (already scaled).  Fills cache slots [0, L).  logits_rows: int32 rows to emit logits for (None = all)."""
         w = self.w
@@ -157,7 +162,7 @@ class PaliGemmaEngine:
         H, I, nh, nkv, hd = w.hidden, w.inter, w.heads, w.kv_heads, w.head_dim
         cos_t, sin_t = self.rope(L + 2)
         xn = self._buf("t_xn", (T, H), torch.bfloat16)
-        qkv = self._buf("t_qkv", (T, w.qkv_n), torch.bfloat16)
+        qb = self._buf("t_q", (T, nh * hd), torch.bfloat16)
         attn = self._buf("t_attn", (T, nh * hd), torch.bfloat16)
         h = self._buf("t_h", (T, I), torch.bfloat16)
         tiles = lambda n: ((T + 127) // 128) * ((n + 127) // 128)  # noqa: E731
@@ -166,13 +171,16 @@ class PaliGemmaEngine:
         part = self._buf("t_part", (max(s_o, s_d), T, H), torch.float32)
         pos = positions.to(device=self.device, dtype=torch.int32).reshape(-1).contiguous()
         ns = 0
+        if taps is not None:
+            taps.append(x_resid.clone())
         kvd = nkv * hd
         for i, Lw in enumerate(w.tl):
             ops.norm_residual(x_resid, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
-            ops.gemm(xn, Lw["qkv_w"], qkv)
-            ops.rope_kv_write(qkv, pos, cos_t, sin_t, cache.k[i], cache.vt[i], T=T, L=L, Hq=nh, Hkv=nkv, D=hd,
-                              Smax=cache.Smax)
-            ops.attention(qkv, w.qkv_n, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+            # q|k|v projection + RoPE + KV-cache append in one GEMM (modeling_gemma.py:274-302)
+            fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=0,
+                                kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
+            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=T)
+            ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
@@ -182,6 +190,8 @@ class PaliGemmaEngine:
             ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
             ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=s_d)
             ns = s_d
+            if taps is not None:
+                taps.append((x_resid + part[:ns].sum(0)).clone())
         cache.length = L
         rows = logits_rows.numel() if logits_rows is not None else T
         xf = self._buf("t_xf", (rows, H), torch.bfloat16)
@@ -208,45 +218,53 @@ class PaliGemmaEngine:
         return st
 
     def decode_step(self, st: dict, cache: KVStore, feats: Optional[torch.Tensor], sampler: dict):
-        """One token for B rows: embed(ids) -> 18 layers -> lm_head -> argmax/top-p (advances the state)."""
+        """One token for B rows: embed(ids) -> 18 layers -> lm_head -> argmax/top-p (advances the state).
+
+        Per layer 5 launches: [RMSNorm + q|k|v GEMV + RoPE + KV append] -> split-KV attention ->
+        [attention merge + o GEMV (split-K partials)] -> [RMSNorm + gate/up GEMV + gelu*mul] ->
+        down GEMV (split-K partials).  The residual stream ping-pongs between two fp32 buffers; the
+        RMSNorm prologues add the previous GEMV's split-K partials (deterministic order)."""
         w = self.w
         B = st["ids"].numel()
         H, I, nh, nkv, hd = w.hidden, w.inter, w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
         cos_t, sin_t = self.rope(cache.Smax + 2)
-        resid = self._buf("d_resid", (B, H), torch.float32)
+        res_a = self._buf("d_res_a", (B, H), torch.float32)
+        res_b = self._buf("d_res_b", (B, H), torch.float32)
         xn = self._buf("d_xn", (B, H), torch.bfloat16)
-        qkv = self._buf("d_qkv", (B, w.qkv_n), torch.bfloat16)
-        attn = self._buf("d_attn", (B, nh * hd), torch.bfloat16)
+        qb = self._buf("d_q", (B, nh * hd), torch.bfloat16)
         h = self._buf("d_h", (B, I), torch.bfloat16)
-        part = self._buf("d_part", (max(self.DECODE_SPLIT_O, self.DECODE_SPLIT_DOWN), B, H), torch.float32)
+        so, sd = self.DECODE_SPLIT_O, self.DECODE_SPLIT_DOWN
+        part = self._buf("d_part", (max(so, sd), B, H), torch.float32)
         SK = self.DECODE_SPLIT_KEYS
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
         dt = (hd + 15) // 16 * 16
         part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
         part_ml = self._buf("d_pml", (B * nkv * nsplit * 16 * 2,), torch.float32)
         logits = self._buf("d_logits", (B, w.vocab), torch.float32)
-        ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, resid,
+        ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, res_a,
                         image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
                         normalizer=float(w.hidden ** 0.5))
         ns = 0
         for i, Lw in enumerate(w.tl):
-            ops.norm_residual(resid, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
-            ops.gemm(xn, Lw["qkv_w"], qkv)
-            ops.rope_kv_write(qkv, st["pos"], cos_t, sin_t, cache.k[i], cache.vt[i], T=B, L=1, Hq=nh, Hkv=nkv,
-                              D=hd, Smax=cache.Smax, slot_dev=st["kv_len"])
-            ops.attention(qkv, w.qkv_n, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
+                                norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
+                                rows_per_batch=1, slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i],
+                                vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
+            ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
-            ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
-            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=self.DECODE_SPLIT_O)
-            ops.norm_residual(resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=self.DECODE_SPLIT_O,
-                              out=xn)
-            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=self.DECODE_SPLIT_DOWN)
-            ns = self.DECODE_SPLIT_DOWN
-        ops.norm_residual(resid, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv)
+            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32, M=B, ksplit=so)
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=so,
+                                norm_w=Lw["post_w"], eps=1e-6)
+            ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=sd)
+            ns = sd
+        ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
         ops.gemm(xn, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
         self.sample(logits, st, sampler, advance=True)
         return logits

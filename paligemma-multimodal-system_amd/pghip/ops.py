@@ -13,7 +13,8 @@ import torch
 
 from . import _lib
 
-EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT = range(6)
+EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE = range(7)
+PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE = range(3)
 NORM_LAYER, NORM_RMS = 0, 1
 
 
@@ -62,6 +63,30 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
         raise ValueError("pghip.gemm: K must be a multiple of 64 for M > 16")
     _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
               _p(aux), aux_rows, _p(aux_out), aux_ld, aux_n, _s())
+    return out
+
+
+def fused_args(**kw) -> "_lib.PgFusedArgs":
+    """Build a PgFusedArgs; tensors are passed as their data pointers."""
+    fa = _lib.PgFusedArgs()
+    for k, v in kw.items():
+        setattr(fa, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+    return fa
+
+
+def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa, *, epi: int = EPI_BF16,
+               M: int, bias: Optional[torch.Tensor] = None, ksplit: int = 1, N: Optional[int] = None,
+               ldc: Optional[int] = None, keep=None) -> torch.Tensor:
+    """pg_gemm_fused: the GEMM with a fused prologue (x produced in-kernel) and/or RoPE/KV epilogue.
+    `fa` is a PgFusedArgs (see fused_args); `keep` holds tensors it points to alive for the call."""
+    _chk(W, torch.bfloat16, "W")
+    N = W.shape[0] if N is None else N
+    K = W.shape[1]
+    if ldc is None:
+        ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
+    lda = A.stride(0) if A is not None else K
+    _lib.call("pg_gemm_fused", _p(A), lda, _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
+              _lib.C.byref(fa), _s())
     return out
 
 

@@ -9,7 +9,8 @@ tensors of any float dtype on any device.  Output, on the HIP device:
            [Ip][hv] (N padded to 64, zero rows), fc2 W [hv][Ip] (K padded), fp32 LN params
   proj     W [P][hv] bf16
   Gemma    embed [V][H] bf16 (gather AND tied lm_head, modeling_gemma.py:492-499), lm_head bias fp32,
-           per layer: qkv W [(nh+2nkv)*hd][H] (q | k | v), o W, gate/up W [2I][H] interleaved in
+           per layer: qkv W [(nh+2nkv)*hd][H] (q | k | v, rows of every head block in rope_row_perm
+           order for the fused RoPE/KV-append epilogue), o W, gate/up W [2I][H] interleaved in
            16-row blocks (gate 16u..16u+15, then up 16u..16u+15) for the fused GELU*mul epilogue,
            down W [H][I], fp32 RMSNorm weights (the kernel applies 1 + w).
 
@@ -22,6 +23,15 @@ import torch
 
 def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+def rope_row_perm(D: int) -> torch.Tensor:
+    """Row order inside one D-wide head block for the fused RoPE epilogue: 16-row tile t holds
+    dims 8t..8t+7 then D/2+8t..D/2+8t+7, so each lane's rotate_half partner is lane ^ 32."""
+    idx = []
+    for t in range(D // 16):
+        idx += [8 * t + j for j in range(8)] + [D // 2 + 8 * t + j for j in range(8)]
+    return torch.tensor(idx, dtype=torch.long)
 
 
 class PackedWeights:
@@ -92,6 +102,10 @@ class PackedWeights:
         self.rope_theta = t.get("rope_theta", 10000.0)
         if self.inter % 16:
             raise ValueError("intermediate_size must be a multiple of 16 for the gate/up interleave")
+        if self.head_dim % 16:
+            raise ValueError("head_dim must be a multiple of 16 for the fused RoPE epilogue")
+        perm = rope_row_perm(self.head_dim).to(dev)
+        nblk = self.heads + 2 * self.kv_heads
         lm = "language_model."
         self.embed = bf(get(lm + "model.embed_tokens.weight"))
         self.lm_bias = f32(get(lm + "lm_head.bias"))
@@ -101,7 +115,8 @@ class PackedWeights:
             lp = f"{lm}model.layers.{i}."
             a = lp + "self_attn."
             qkv_w = torch.cat([bf(get(a + "q_proj.weight")), bf(get(a + "k_proj.weight")),
-                               bf(get(a + "v_proj.weight"))], 0).contiguous()
+                               bf(get(a + "v_proj.weight"))], 0)
+            qkv_w = qkv_w.view(nblk, self.head_dim, H)[:, perm, :].reshape(nblk * self.head_dim, H).contiguous()
             g = bf(get(lp + "mlp.gate_proj.weight")).reshape(I // 16, 16, H)
             u = bf(get(lp + "mlp.up_proj.weight")).reshape(I // 16, 16, H)
             gu = torch.stack([g, u], dim=1).reshape(2 * I, H).contiguous()

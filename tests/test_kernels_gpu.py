@@ -136,9 +136,10 @@ def test_attention_vision_layout(B, N, nh, hd):
     hv = nh * hd
     M = B * N
     qkv = rnd(M, 3 * hv, seed=10)
-    vt = qkv[:, 2 * hv:].t().contiguous()
+    vt = torch.zeros(hv, M + 32, dtype=torch.bfloat16, device="cuda")
+    vt[:, :M] = qkv[:, 2 * hv:].t()
     o = torch.empty(M, hv, dtype=torch.bfloat16, device="cuda")
-    ops.attention(qkv, 3 * hv, o, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * M, M,
+    ops.attention(qkv, 3 * hv, o, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
                   B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=hd ** -0.5)
     x = qkv.view(B, N, 3, nh, hd).permute(2, 0, 3, 1, 4)
     ref = _attn_ref(x[0], x[1], x[2], hd ** -0.5).permute(0, 2, 1, 3).reshape(M, hv)
@@ -278,3 +279,88 @@ def test_topp_matches_reference_filter(golden):
             assert got in kept
             if kept == ref_kept:
                 assert got == want, (ci, k, got, want)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+def test_gemm_fused_rmsnorm_prologue(M):
+    """x = RMSNorm(resid + sum partials)*(1+w) built in-kernel; resid_out written once."""
+    from pghip import ops
+    K, N, S = 2048, 512, 4
+    resid = torch.randn(M, K).cuda()
+    part = torch.randn(S, M, K).cuda() * 0.5
+    w = torch.randn(K).cuda() * 0.1
+    W = rnd(N, K, scale=1 / 45, seed=20)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    rout = torch.zeros(M, K).cuda()
+    fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=resid, resid_out=rout, partials=part, nsplit=S,
+                        norm_w=w, eps=1e-6)
+    ops.gemm_fused(None, W, out, fa, epi=ops.EPI_BF16, M=M)
+    x = resid + part.sum(0)
+    xn = (x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)).to(torch.bfloat16).float()
+    assert err(rout, x) < 1e-6
+    assert err(out, xn @ W.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_gemm_fused_attention_merge_prologue(B):
+    """o_proj GEMV whose prologue merges split-KV attention partials == attention+combine+GEMV."""
+    from pghip import ops
+    nh, nkv, hd, L, Smax = 8, 1, 256, 200, 256
+    kvd = nkv * hd
+    q = rnd(B, nh * hd, seed=21)
+    kc, vtc = rnd(B, Smax, kvd, seed=22), rnd(B, kvd, Smax, seed=23)
+    lkv = torch.tensor([L], dtype=torch.int32, device="cuda")
+    SK, nsplit, dt = 32, 8, 256
+    po = torch.empty(B * nkv * nsplit * 16 * dt, device="cuda")
+    pml = torch.empty(B * nkv * nsplit * 16 * 2, device="cuda")
+    ops.attention(q, nh * hd, None, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
+                  B=B, Lq=1, Lkv=0, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=SK,
+                  nsplit=nsplit, part_o=po, part_ml=pml)
+    ref_o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
+    ops.attn_combine(po, pml, ref_o, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+    Wo = rnd(2048, nh * hd, scale=1 / 45, seed=24)
+    for z in (1, 2):
+        part = torch.empty(z, B, 2048, device="cuda")
+        fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=po, part_ml=pml, asplit=nsplit, head_dim=hd,
+                            dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv)
+        ops.gemm_fused(None, Wo, part, fa, epi=ops.EPI_F32, M=B, ksplit=z)
+        assert err(part.sum(0), ref_o.float() @ Wo.float().t()) < 1e-2
+    # and the attention itself against a float reference
+    kf = kc[:, :L].float()
+    vf = vtc[:, :, :L].float().transpose(1, 2)
+    s = torch.einsum("bhd,bkd->bhk", q.view(B, nh, hd).float(), kf) * hd ** -0.5
+    ref = torch.einsum("bhk,bkd->bhd", torch.softmax(s, -1), vf).reshape(B, -1)
+    assert err(ref_o, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,L", [(1, 1), (3, 1), (40, 20), (264, 264)])
+def test_gemm_fused_qkv_rope_epilogue(M, L):
+    """q|k|v GEMM with RoPE + KV append in the epilogue == plain GEMM + pg_rope_kv_write."""
+    from pghip import engine, ops
+    from pghip.weights import rope_row_perm
+    nh, nkv, hd, H, Smax = 8, 1, 256, 512, 320
+    nblk = nh + 2 * nkv
+    W = rnd(nblk * hd, H, scale=1 / 22, seed=25)
+    Wp = W.view(nblk, hd, H)[:, rope_row_perm(hd).cuda(), :].reshape(nblk * hd, H).contiguous()
+    x = rnd(M, H, seed=26)
+    B = M // L
+    pos = (torch.arange(M) % L + 7).to(torch.int32).cuda()
+    cos_t, sin_t = engine.rope_tables(hd, 1024, 10000.0, "cuda")
+    slot = torch.tensor([5], dtype=torch.int32, device="cuda")
+    # reference path
+    qkv = torch.empty(M, nblk * hd, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(x, W, qkv)
+    kc_r = torch.zeros(B, Smax, nkv * hd, dtype=torch.bfloat16, device="cuda")
+    vt_r = torch.zeros(B, nkv * hd, Smax, dtype=torch.bfloat16, device="cuda")
+    ops.rope_kv_write(qkv, pos, cos_t, sin_t, kc_r, vt_r, T=M, L=L, Hq=nh, Hkv=nkv, D=hd, Smax=Smax, slot_base=3,
+                      slot_dev=slot)
+    # fused
+    q = torch.empty(M, nh * hd, dtype=torch.bfloat16, device="cuda")
+    kc = torch.zeros_like(kc_r)
+    vt = torch.zeros_like(vt_r)
+    fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_dev=slot, slot_base=3,
+                        kc=kc, vtc=vt, smax=Smax, q_heads=nh, kv_heads=nkv)
+    ops.gemm_fused(x, Wp, q, fa, epi=ops.EPI_QKV_ROPE, M=M)
+    assert err(q, qkv[:, :nh * hd]) < 1e-2
+    assert err(kc, kc_r) < 1e-2
+    assert err(vt, vt_r) < 1e-2
