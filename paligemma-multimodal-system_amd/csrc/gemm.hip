@@ -75,6 +75,10 @@ struct EpiArgs {
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
 // the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).
 __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
+  if (e.bias && n0 < e.N) {                           // bias in packed (permuted) column order
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += e.bias[n0 + j];
+  }
   f32x4 pr;
 #pragma unroll
   for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);

@@ -63,7 +63,7 @@ class PaliGemmaEngine:
         self.cfg = cfg
         self.w = weights
         self.device = torch.device(device)
-        self.image_token_id = cfg["image_token_index"]
+        self.image_token_id = cfg.get("image_token_index", 256000)
         pad = cfg.get("pad_token_id")
         self.pad_id = -1 if pad is None else pad
         self.n_img = weights.n_img
@@ -136,7 +136,9 @@ class PaliGemmaEngine:
         hid = torch.empty(M, hv, dtype=torch.float32, device=self.device) if want_hidden else None
         ops.norm_residual(resid, w.post_w, b=w.post_b, mode=ops.NORM_LAYER, eps=w.v_eps, partials=part, nsplit=ns,
                           out=xn, out_f32=hid)
-        feats = torch.empty(M, w.proj_dim, dtype=torch.float32, device=self.device)
+        feats = torch.empty(M, max(w.proj_dim, 1), dtype=torch.float32, device=self.device)
+        if w.proj_w is None:                                              # vision-only pack
+            return (None, hid) if want_hidden else None
         ops.gemm(xn, w.proj_w, feats, epi=ops.EPI_F32)
         return (feats, hid) if want_hidden else feats
 
@@ -266,7 +268,8 @@ class PaliGemmaEngine:
             ns = sd
         ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
         ops.gemm(xn, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
-        self.sample(logits, st, sampler, advance=True)
+        if sampler is not None:
+            self.sample(logits, st, sampler, advance=True)
         return logits
 
     def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool):

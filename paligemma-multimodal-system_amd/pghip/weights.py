@@ -35,10 +35,11 @@ def rope_row_perm(D: int) -> torch.Tensor:
 
 
 class PackedWeights:
-    def __init__(self, cfg: dict, get, device="cuda"):
+    def __init__(self, cfg: dict, get, device="cuda", parts=("vision", "proj", "text")):
         self.cfg = cfg
         self.device = torch.device(device)
-        v, t = cfg["vision_config"], cfg["text_config"]
+        self.parts = tuple(parts)
+        v, t = cfg["vision_config"], cfg.get("text_config")
         dev = self.device
 
         def bf(x):
@@ -47,6 +48,14 @@ class PackedWeights:
         def f32(x):
             return x.detach().to(device=dev, dtype=torch.float32).contiguous()
 
+        self.vl, self.tl = [], []
+        self.proj_w, self.proj_dim = None, 0
+        if "vision" in self.parts:
+            self._pack_vision(v, get, dev, bf, f32)
+        if "text" in self.parts:
+            self._pack_text(t, get, dev, bf, f32)
+
+    def _pack_vision(self, v, get, dev, bf, f32):
         # ---------------- SigLIP
         hv, iv = v["hidden_size"], v["intermediate_size"]
         self.v_hidden, self.v_heads = hv, v["num_attention_heads"]
@@ -88,9 +97,10 @@ class PackedWeights:
                 fc1_w=fc1_w, fc1_b=fc1_b, fc2_w=fc2_w, fc2_b=f32(get(lp + "mlp.fc2.bias"))))
         self.post_w = f32(get(pre + "post_layernorm.weight"))
         self.post_b = f32(get(pre + "post_layernorm.bias"))
-        self.proj_w = bf(get("multi_modal_projector.linear.weight"))
-        self.proj_dim = self.proj_w.shape[0]
+        self.proj_w = bf(get("multi_modal_projector.linear.weight")) if "proj" in self.parts else None
+        self.proj_dim = self.proj_w.shape[0] if self.proj_w is not None else 0
 
+    def _pack_text(self, t, get, dev, bf, f32):
         # ---------------- Gemma
         self.hidden = t["hidden_size"]
         self.heads = t["num_attention_heads"]

@@ -1,0 +1,113 @@
+"""CPU-side checks: drop-in API surface, state-dict key parity, configs/recipes, the C-ABI library's
+exported symbols, host pre-processing vs the reference's own outputs, and no CPU fallback."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT
+
+from oracle import configs as ocfg, synth
+
+
+def _tiny_model():
+    from modeling_paligemma import PaliGemmaConfig, PaliGemmaForConditionalGeneration
+    return PaliGemmaForConditionalGeneration(PaliGemmaConfig(**ocfg.TINY))
+
+
+def test_state_dict_keys_equal_reference_layout():
+    m = _tiny_model()
+    keys = set(m.state_dict().keys())
+    want = set(synth.state_dict_shapes(ocfg.TINY)) | {"language_model.lm_head.weight"}
+    assert keys == want
+    sd = m.state_dict()
+    for k, shp in synth.state_dict_shapes(ocfg.TINY).items():
+        assert tuple(sd[k].shape) == tuple(shp), k
+
+
+def test_reference_checkpoint_loads_strict_false_and_ties():
+    m = _tiny_model()
+    sd = {k: torch.from_numpy(v) for k, v in synth.generate_state_dict(ocfg.TINY).items()}
+    res = m.load_state_dict(sd, strict=False)
+    assert set(res.missing_keys) == {"language_model.lm_head.weight"} and not res.unexpected_keys
+    m.tie_weights()
+    assert m.language_model.lm_head.weight is m.language_model.model.embed_tokens.weight
+
+
+def test_configs_and_recipes_match_oracle():
+    from pghip import configs, synthetic
+    assert configs.CONFIGS == ocfg.CONFIGS
+    for name in ("pt-224", "tiny"):
+        shapes = synth.state_dict_shapes(ocfg.CONFIGS[name])
+        assert synthetic.state_dict_shapes(configs.CONFIGS[name]) == shapes
+        for k, s in shapes.items():
+            assert synthetic.recipe(k, s) == synth.recipe(k, s), k
+            assert synthetic.seed_of(k) == synth.seed_of(k), k
+
+
+def test_library_exports_every_header_symbol():
+    from pghip import _lib
+    hdr = open(os.path.join(ROOT, "include", "pghip.h")).read()
+    declared = set(re.findall(r"^int (pg_\w+)\(", hdr, re.M))
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    lib = _lib.load()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.pg_abi_version() == 1
+
+
+def test_no_cpu_fallback():
+    m = _tiny_model()
+    ids = torch.tensor([[299] * 16 + [2, 5, 108]])
+    with pytest.raises(RuntimeError, match="HIP"):
+        m(input_ids=ids, pixel_values=torch.zeros(1, 3, 56, 56), attention_mask=torch.ones_like(ids))
+    from modeling_gemma import GemmaMLP, GemmaConfig
+    mlp = GemmaMLP(GemmaConfig(hidden_size=128, intermediate_size=320))
+    with pytest.raises(RuntimeError, match="HIP"):
+        mlp(torch.zeros(1, 2, 128))
+
+
+@pytest.mark.parametrize("name", ["tiny", "pt224"])
+def test_process_images_matches_reference(golden, name):
+    """Host pre-processing against pixel values the reference's process_images made."""
+    from PIL import Image
+    from processing_paligemma import process_images
+    g = golden(name)
+    imgs = g["images_u8"] if "images_u8" in g else g["b1_images_u8"]
+    want = g["pixel_values"] if "pixel_values" in g else g["b1_pixel_values"]
+    got = np.stack(process_images([Image.fromarray(im) for im in imgs], imgs.shape[1], 1 / 255.0,
+                                  Image.Resampling.BICUBIC))
+    assert np.array_equal(got.astype(np.float32), want)
+
+
+def test_gemma_string_list_repr_quirk():
+    from processing_paligemma import create_gemma_string
+    assert create_gemma_string(["caption en"], 2, "<image>", "<bos>") == "<image><image><bos>['caption en']\n"
+
+
+def test_hf_key_remap():
+    from utils import remap_hf_key
+    assert remap_hf_key("vision_tower.vision_model.encoder.layers.3.self_attn.q_proj.weight") == \
+        "vision_tower.model.encoder.layers.3.self_attn.query_proj.weight"
+    assert remap_hf_key("vision_tower.vision_model.embeddings.position_embedding.weight") == \
+        "vision_tower.model.embeddings.positional_embeddings.weight"
+    assert remap_hf_key("language_model.model.layers.0.self_attn.q_proj.weight") == \
+        "language_model.model.layers.0.self_attn.q_proj.weight"
+
+
+def test_kvcache_reference_api_on_static_store():
+    from modeling_gemma import KVCache
+    kv = KVCache()
+    assert kv.num_items() == 0
+    k = torch.randn(2, 1, 5, 32)
+    v = torch.randn(2, 1, 5, 32)
+    K, V = kv.update(k, v, 0)
+    kv.update(k, v, 1)
+    assert kv.num_items() == 5 and K.shape == (2, 1, 5, 32)
+    K2, V2 = kv.update(k[:, :, :1], v[:, :, :1], 0)
+    assert K2.shape == (2, 1, 6, 32)
+    assert torch.allclose(K2[:, :, :5].float(), k.to(torch.bfloat16).float())
+    assert torch.allclose(V2[:, :, 5].float(), v[:, :, 0].to(torch.bfloat16).float())
+    assert len(kv.k_cache) == 2 and kv.v_cache[1].shape == (2, 1, 5, 32)
