@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int R = a.Lq * a.G;
   const int D = a.D;
 
-  const int r0 = split ? 0 : (blockIdx.x * 64 + wave * 16);
+  const int r0 = split ? 0 : (blockIdx.x * (int)(blockDim.x >> 6) + wave) * 16;
   int kbeg = 0, kend = Lkv, sp = 0;
   if (split) {
     sp = sg * 4 + wave;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 
 #define ATTN_DISPATCH(DP_, DT_)                                                             \
   if (DP == DP_ && DT == DT_) {                                                              \
-    hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);              \
+    hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(split_keys > 0 ? 256 : 64), 0, stream, a); \
     launched = true;                                                                         \
   }
 
@@ -268,7 +268,7 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
     PG_REQUIRE(Lq * G <= 16 && nsplit % 4 == 0 && part_o && part_ml && split_keys % 32 == 0);
     grid = dim3(1, Hkv * (nsplit / 4), B);
   } else {
-    grid = dim3((Lq * G + 63) / 64, Hkv, B);
+    grid = dim3((Lq * G + 15) / 16, Hkv, B);   // one wave (16 query rows) per workgroup: 4x the workgroups
   }
   bool launched = false;
   ATTN_DISPATCH(32, 1)

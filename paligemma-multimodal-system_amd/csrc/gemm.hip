@@ -58,6 +58,15 @@ struct PgFusedArgs {
   int q_heads;
 };
 
+// 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
+__device__ __forceinline__ f32x4 load4_guard(const float* __restrict__ p, int n0, int N) {
+  if (n0 + 3 < N) return *(const f32x4*)(p + n0);
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) if (n0 + j < N) v[j] = p[n0 + j];
+  return v;
+}
+
 struct EpiArgs {
   const float* bias;
   void* C;
@@ -75,10 +84,7 @@ struct EpiArgs {
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
 // the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).
 __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
-  if (e.bias && n0 < e.N) {                           // bias in packed (permuted) column order
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] += e.bias[n0 + j];
-  }
+  if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);   // bias in packed (permuted) column order
   f32x4 pr;
 #pragma unroll
   for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
@@ -122,13 +128,10 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
 // Store 4 consecutive columns n0..n0+3 of row m (values v).  z = split index.
 template <int EPI>
 __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x4 v, int z) {
-  if (m >= e.M) return;
+  if (m >= e.M || n0 >= e.N) return;
+  if (e.bias && (EPI != PG_EPI_F32 || z == 0)) v += load4_guard(e.bias, n0, e.N);
   if constexpr (EPI == PG_EPI_F32) {
     float* C = (float*)e.C + (size_t)z * e.M * e.ldc + (size_t)m * e.ldc;
-    if (e.bias && z == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) if (n0 + j < e.N) v[j] += e.bias[n0 + j];
-    }
     if (n0 + 3 < e.N) {
       *(f32x4*)(C + n0) = v;
     } else {
@@ -137,21 +140,18 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x
     }
   } else if constexpr (EPI == PG_EPI_F32_POS) {
     float* C = (float*)e.C + (size_t)m * e.ldc;
-    const float* P = e.aux + (size_t)(m % e.aux_rows) * e.ldc;
+    v += load4_guard(e.aux + (size_t)(m % e.aux_rows) * e.ldc, n0, e.N);
+    if (n0 + 3 < e.N) {
+      *(f32x4*)(C + n0) = v;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int n = n0 + j;
-      if (n < e.N) C[n] = v[j] + e.bias[n] + P[n];
+      for (int j = 0; j < 4; ++j) if (n0 + j < e.N) C[n0 + j] = v[j];
     }
   } else {
     // bf16 outputs
+    if constexpr (EPI == PG_EPI_BF16_GELU) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int n = n0 + j;
-      float x = v[j];
-      if (e.bias && n < e.N) x += e.bias[n];
-      if constexpr (EPI == PG_EPI_BF16_GELU) x = gelu_tanh(x);
-      v[j] = x;
+      for (int j = 0; j < 4; ++j) v[j] = gelu_tanh(v[j]);
     }
     if constexpr (EPI == PG_EPI_BF16_VT) {
       if (n0 >= e.aux_n) {
@@ -189,17 +189,24 @@ __device__ __forceinline__ void epi_gelu_mul4(const EpiArgs& e, int m, int gb, i
 // --------------------------------------------------------------------------------------
 // Tiled GEMM (prefill)
 // --------------------------------------------------------------------------------------
-#define TBM 128
+// BM x 128 output tile, BK = 64, 4 waves (BM=128: 2x2 waves of 64x64; BM=96: 2x2 of 48x64;
+// BM=64: 1x4 waves of 64x32).
+// A and W k-tiles are staged HBM->LDS with global_load_lds (16 B/lane, 1 KiB pieces of 8 rows x
+// 128 B, XOR-swizzled through the SOURCE address) into an STAGES-deep ring; the wait for stage kt
+// is a counted vmcnt (the younger stages stay in flight across the raw s_barrier), so each k-step's
+// MFMAs overlap the next STAGES-1 stages' loads.  One __shared__ array only (a second one makes
+// hipcc drain vmcnt before every ds_read).
 #define TBN 128
 #define TBK 64
-#define TILE_BYTES (TBM * TBK * 2)   // 16 KiB per operand tile
 
-// Stage a 128-row x 64-k bf16 tile into LDS (lane-linear 1 KiB pieces, XOR swizzle on the source).
+// Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread over the 4 waves.
+template <int ROWS>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int rows_valid,
                                            int k0, char* lds_tile, int wave, int lane) {
+  constexpr int PER_WAVE = ROWS / 32;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int blk = wave * 4 + it;                 // 1 KiB piece = 8 rows x 128 B
+  for (int it = 0; it < PER_WAVE; ++it) {
+    const int blk = wave * PER_WAVE + it;          // 1 KiB piece = 8 rows x 128 B
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);     // logical 16-B chunk landing at physical chunk lane&7
     int gr = row0 + r;
@@ -214,14 +221,35 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
   return *(const bf16x8*)(tile + row * 128 + phys * 16);
 }
 
-template <int EPI>
+__device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [0, 24]
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int EPI, int BM, int STAGES>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W, int ldw, int K, int kchunk,
                                                         int tiles_m, int tiles_n, EpiArgs e) {
-  __shared__ __attribute__((aligned(1024))) char smem[4 * TILE_BYTES];   // 2 buffers x (A, W)
+  constexpr int A_BYTES = BM * TBK * 2;
+  constexpr int W_BYTES = TBN * TBK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + W_BYTES;
+  constexpr int P = BM / 32 + TBN / 32;            // glds pieces per wave per stage
+  constexpr int WN = BM == 64 ? 4 : 2;             // waves along N
+  constexpr int WM = 4 / WN;                       // waves along M
+  constexpr int NI = BM / WM / 16;                 // 16-row subtiles per wave
+  constexpr int NJ = TBN / WN / 16;                // 16-col subtiles per wave
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped tile order.
   const int nwg = gridDim.x;
@@ -236,67 +264,66 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
   const int gsize = min(tiles_m - first_m, GROUP);
   const int tm = first_m + (pid % gsize);
   const int tn = (pid % (GROUP * tiles_n)) / gsize;
-  const int m0 = tm * TBM, n0 = tn * TBN;
+  const int m0 = tm * BM, n0 = tn * TBN;
 
   const int z = blockIdx.z;
   const int kbeg = z * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  const int nk = (kend - kbeg) / TBK;
+  const int nk = max(0, (kend - kbeg) / TBK);
 
-  f32x4 acc[4][4];
+  f32x4 acc[NI][NJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // buffer b: A tile at smem + 2b*TILE_BYTES, W tile right after it
-  if (nk > 0) {
-    stage_tile(A, lda, m0, e.M, kbeg, smem, wave, lane);
-    stage_tile(W, ldw, n0, e.N, kbeg, smem + TILE_BYTES, wave, lane);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % STAGES) * STAGE_BYTES;
+    stage_tile<BM>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
+    stage_tile<TBN>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
+  };
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s);
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    char* nxt = smem + (cur ^ 1) * 2 * TILE_BYTES;
-    if (kt + 1 < nk) {
-      stage_tile(A, lda, m0, e.M, kbeg + (kt + 1) * TBK, nxt, wave, lane);
-      stage_tile(W, ldw, n0, e.N, kbeg + (kt + 1) * TBK, nxt + TILE_BYTES, wave, lane);
-    }
-    const char* tA = smem + cur * 2 * TILE_BYTES;
-    const char* tW = tA + TILE_BYTES;
+    // stage kt has landed once at most (issued stages after kt) * P pieces are outstanding
+    const int younger = min(nk - 1, kt + STAGES - 2) - kt;
+    wait_vm(younger * P);
+    __builtin_amdgcn_s_barrier();                  // every wave's pieces of kt landed; kt-1 fully read
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+    const char* tA = smem + (kt % STAGES) * STAGE_BYTES;
+    const char* tW = tA + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int chunk = s * 4 + (lane >> 4);
-      bf16x8 fa[4], fw[4];
+      bf16x8 fa[NI], fw[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = lds_frag(tA, wm * 64 + i * 16 + (lane & 15), chunk);
+      for (int i = 0; i < NI; ++i) fa[i] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fw[j] = lds_frag(tW, wn * 64 + j * 16 + (lane & 15), chunk);
+      for (int j = 0; j < NJ; ++j) fw[j] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fw[j], fa[i], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(fw[j], fa[i], acc[i][j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
-  // epilogue: acc[i][j] lane holds C[m = m0+wm*64+i*16+(lane&15)][n = n0+wn*64+j*16+4*(lane>>4) + 0..3]
+  // epilogue: acc[i][j] lane holds C[m = m0+wm*(BM/WM)+i*16+(lane&15)][n = n0+wn*(128/WN)+j*16+4*(lane>>4) + 0..3]
   const int q = 4 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+  for (int i = 0; i < NI; ++i) {
+    const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    const int nb = n0 + wn * (TBN / WN);
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
 #pragma unroll
-      for (int j = 0; j < 4; j += 2) epi_gelu_mul4(e, m, n0 + wn * 64 + j * 16, q, acc[i][j], acc[i][j + 1]);
+      for (int j = 0; j < NJ; j += 2) epi_gelu_mul4(e, m, nb + j * 16, q, acc[i][j], acc[i][j + 1]);
     } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) epi_qkv_rope4(e, m, n0 + wn * 64 + j * 16 + q, acc[i][j]);
+      for (int j = 0; j < NJ; ++j) epi_qkv_rope4(e, m, nb + j * 16 + q, acc[i][j]);
     } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) epi_store4<EPI>(e, m, n0 + wn * 64 + j * 16 + q, acc[i][j], z);
+      for (int j = 0; j < NJ; ++j) epi_store4<EPI>(e, m, nb + j * 16 + q, acc[i][j], z);
     }
   }
 }
@@ -543,13 +570,25 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 // --------------------------------------------------------------------------------------
 // C ABI
 // --------------------------------------------------------------------------------------
+// Tile choice: 128-row tiles (2-stage ring, 64 KiB LDS -> 2 workgroups per CU) when that grid already
+// has >= 256 workgroups; otherwise 64-row tiles with a 4-stage ring.  Split-K (fp32 partial epilogue
+// only) is chosen by the caller.
 template <int EPI>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
-  const int tiles_m = (e.M + TBM - 1) / TBM, tiles_n = (e.N + TBN - 1) / TBN;
+  const int tiles_n = (e.N + TBN - 1) / TBN;
   int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
-  dim3 grid(tiles_m * tiles_n, 1, ksplit);
-  hipLaunchKernelGGL(gemm_tile_kernel<EPI>, grid, dim3(256), 0, st, A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
+  const int t128 = ((e.M + 127) / 128) * tiles_n;
+  if (t128 >= 256) {
+    const int tiles_m = (e.M + 127) / 128;
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st, A,
+                       lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
+    return;
+  }
+  // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
+  const int m64 = (e.M + 63) / 64;
+  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda, W,
+                     ldw, K, kchunk, m64, tiles_n, e);
 }
 
 // measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;

@@ -163,7 +163,7 @@ def synth_fill(out: torch.Tensor, seedmix: int, a: float, mean: float):
     _lib.call("pg_synth_fill", _p(out), out.numel(), seedmix & 0xFFFFFFFF, float(a), float(mean), kind, _s())
 
 
-def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 16) -> int:
+def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -> int:
     """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
     s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))
     return s
