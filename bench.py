@@ -6,7 +6,10 @@ merge -> Gemma prefill -> 128 greedy tokens (graph-replayed decode steps; EOS ig
 token count is fixed).  value = generated tokens / step wall time over all ranks.
 
 Multi-GPU (torch.distributed.run, one rank per GPU): --parallel dp (default) runs one request per
-rank (independent replicas, weak scaling); value = all ranks' tokens / max-over-ranks time.
+rank (independent replicas, weak scaling; no data-path collective); value = all ranks' tokens /
+max-over-ranks time.  --parallel tp shards the Gemma decoder over all ranks (q heads, gate/up
+columns, vocabulary; RCCL SUM all-reduce after o_proj and down_proj) and runs ONE
+request across them (strong scaling: per-token latency); value = that request's tokens / time.
 
 Extra fields: prefill_ms, decode_tok_s, decode HBM fraction; "roofline" for the dominant
 kernel (the decode gate/up GEMV, HIP events on the stream it runs on); "cpu_baseline" = the
@@ -119,25 +122,38 @@ def main():
     ap.add_argument("--config", default="pt-224")
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--gen-tokens", type=int, default=128)
-    ap.add_argument("--parallel", default="dp", choices=["dp"])
+    ap.add_argument("--parallel", default="dp", choices=["dp", "tp"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # PG_BENCH_BACKEND=gloo rehearses the multi-rank code paths with several ranks on one GPU
+    backend = os.environ.get("PG_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from pghip import configs, engine, synthetic, weights
     cfg = configs.CONFIGS[args.config]
     B, T = args.batch, args.gen_tokens
     t0 = time.perf_counter()
     sd = synthetic.SyntheticStateDict(cfg)
-    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+    tp = world if args.parallel == "tp" else 1
+    if tp > 1:
+        from pghip.tp import TPComm
+        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=tp),
+                                     comm=TPComm())
+    else:
+        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: weights generated+packed in {time.perf_counter() - t0:.1f}s "
         f"({eng.w.nbytes() / 1e9:.2f} GB)")
@@ -158,7 +174,15 @@ def main():
         return st
 
     st = setup()
-    replay = eng._graph_step(st, state["cache"], state["feats"], dict(do_sample=False))
+    try:
+        replay = eng._graph_step(st, state["cache"], state["feats"], dict(do_sample=False))
+    except Exception as e:  # collectives that cannot be captured: eager decode steps
+        log(f"[bench] rank {rank}: decode-step capture failed ({e}); running eager steps")
+        torch.cuda.synchronize()
+        replay = lambda: eng.decode_step(state["st"], state["cache"], state["feats"], dict(do_sample=False))  # noqa
+        graph_mode = "eager"
+    else:
+        graph_mode = "hipgraph"
     graph_cache = state["cache"]
 
     def request():
@@ -199,7 +223,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     ms_per_step = elapsed / args.steps * 1e3
-    tokens = B * T * args.steps * world
+    tokens = B * T * args.steps * (world // tp)
     value = tokens / elapsed
 
     # prefill-only and decode-only timings (same stream, events)
@@ -228,6 +252,7 @@ def main():
 
     kern_s, kern_bytes = time_dominant_kernel(eng)
     achieved = kern_bytes / kern_s / 1e9
+    kern_desc = f"gemv_kernel<GELU_MUL,2> (decode gate/up, 2x{eng.w.inter}x{eng.w.hidden} bf16)"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -243,11 +268,12 @@ def main():
             "metric": "image->text tokens/s (PaliGemma-3B-224, greedy, 128 new tokens) + prefill ms",
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights of the "
+            "scaling": "weak" if tp == 1 else "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights of the "
             "PaliGemma-3B architecture, name-seeded; random 224x224 image; 8-token prompt)",
             "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
                                    f"{T} greedy tokens (BASELINE.json configs[1])",
-                       "global_batch": B * world, "seq_len": L + T, "parallelism": f"dp{world}"},
+                       "global_batch": B * (world // tp), "seq_len": L + T,
+                       "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}", "decode": graph_mode},
             "prefill_ms": round(prefill_ms, 3),
             "prefill_tflops": round(pf_flops / (prefill_ms / 1e3) / 1e12, 2),
             "prefill_mfma_frac": round(pf_flops / (prefill_ms / 1e3) / 1e12 / BF16_PEAK_TFS, 4),
@@ -257,7 +283,7 @@ def main():
             "decode_hbm_frac": round(decode_hbm / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "gemv_kernel<GELU_MUL,2> (decode gate/up, 2x16384x2048 bf16)",
+                         "kernel": kern_desc,
                          "kernel_avg_us": round(kern_s * 1e6, 2), "bytes_per_launch": kern_bytes},
             "cpu_baseline": cpu,
         }

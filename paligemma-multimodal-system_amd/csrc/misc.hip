@@ -251,6 +251,62 @@ __global__ __launch_bounds__(64) void argmax_final_kernel(const float* __restric
   }
 }
 
+// vocabulary-parallel greedy (tensor parallelism): the local (max, first index + vocab_offset) per row,
+// as float pairs [B][2] to be all-gathered; then pg_argmax_merge picks the global winner.
+__global__ __launch_bounds__(64) void argmax_pairs_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                          int B, int vocab_offset, float* __restrict__ pairs) {
+  const int lane = threadIdx.x;
+  for (int b = 0; b < B; ++b) {
+    float bv = pv[b * AM_CHUNKS + lane];
+    int bi = pi[b * AM_CHUNKS + lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float ov = __shfl_xor(bv, o, 64);
+      int oi = __shfl_xor(bi, o, 64);
+      am_better(bv, bi, ov, oi);
+    }
+    if (lane == 0) { pairs[2 * b] = bv; pairs[2 * b + 1] = (float)(bi + vocab_offset); }
+  }
+}
+
+// pairs [world][B][2] (rank-major, ascending vocabulary ranges): max value, lowest global index on ties
+__global__ void argmax_merge_kernel(const float* __restrict__ pairs, int world, int B, int64_t* __restrict__ out_ids,
+                                    int64_t* __restrict__ hist, int* __restrict__ step, int* __restrict__ pos,
+                                    int* __restrict__ kv_len) {
+  if (threadIdx.x != 0) return;
+  const int st = step ? *step : 0;
+  for (int b = 0; b < B; ++b) {
+    float bv = -INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int r = 0; r < world; ++r) am_better(bv, bi, pairs[(r * B + b) * 2], (int)pairs[(r * B + b) * 2 + 1]);
+    out_ids[b] = bi;
+    if (hist) hist[(long)st * B + b] = bi;
+    if (pos) pos[b] += 1;
+  }
+  if (kv_len) *kv_len += 1;
+  if (step) *step = st + 1;
+}
+
+extern "C" int pg_argmax_pairs(const float* logits, long ld, int B, int V, int vocab_offset, void* workspace,
+                               float* pairs, hipStream_t stream) {
+  PG_REQUIRE(B > 0 && V > 0 && ld % 4 == 0 && vocab_offset >= 0 && vocab_offset + V < (1 << 24));
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + B * AM_CHUNKS);
+  hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
+  hipLaunchKernelGGL(argmax_pairs_kernel, dim3(1), dim3(64), 0, stream, pv, pi, B, vocab_offset, pairs);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int* step,
+                               int* pos, int* kv_len, hipStream_t stream) {
+  PG_REQUIRE(world > 0 && B > 0);
+  hipLaunchKernelGGL(argmax_merge_kernel, dim3(1), dim3(64), 0, stream, pairs, world, B, out_ids, hist, step, pos,
+                     kv_len);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
 // workspace: >= B * AM_CHUNKS * 8 bytes
 extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
                          int64_t* hist, int* step, int* pos, int* kv_len, hipStream_t stream) {

@@ -18,6 +18,12 @@ Output-invariant deviations from the reference: the vision
 tower runs once per request instead of on every call (modeling_paligemma.py:281);
 the KV cache is a static in-place buffer instead of torch.cat (modeling_gemma.py:54-55);
 the generation loop computes only last-position logits.
+
+Tensor parallelism (PackedWeights(tp_rank, tp_world) + a TPComm): every rank runs the same
+kernel sequence on its head / intermediate / vocabulary slice; partial sums of o_proj and
+down_proj are completed by one SUM all-reduce each (they already flow as split-K fp32
+partials, so the next RMSNorm prologue reduces them unchanged), greedy decoding combines
+per-rank (max, index) pairs, and full logits are assembled by a zero-padded all-reduce.
 """
 from __future__ import annotations
 
@@ -27,6 +33,7 @@ from typing import Optional
 import torch
 
 from . import ops
+from .tp import SoloComm
 from .weights import PackedWeights
 
 
@@ -59,9 +66,15 @@ class PaliGemmaEngine:
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
 
-    def __init__(self, cfg: dict, weights: PackedWeights, device="cuda"):
+    def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
         self.w = weights
+        self.comm = comm if comm is not None else SoloComm()
+        self.tp = getattr(weights, "tp_world", 1)
+        if self.comm.world != self.tp:
+            raise ValueError(f"weights packed for tp_world={self.tp}, communicator has world {self.comm.world}")
+        self.split_o = self.DECODE_SPLIT_O if self.tp == 1 else 1        # smaller all-reduce messages under TP
+        self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         self.device = torch.device(device)
         self.image_token_id = cfg.get("image_token_index", 256000)
         pad = cfg.get("pad_token_id")
@@ -188,9 +201,11 @@ class PaliGemmaEngine:
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
                           mask_rs=(mask.stride(-2) if mask is not None else 0))
             ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=s_o)
+            self._allreduce(part[:s_o])
             ops.norm_residual(x_resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=s_o, out=xn)
             ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
             ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=s_d)
+            self._allreduce(part[:s_d])
             ns = s_d
             if taps is not None:
                 taps.append((x_resid + part[:ns].sum(0)).clone())
@@ -200,11 +215,31 @@ class PaliGemmaEngine:
         hid = torch.empty(rows, H, dtype=torch.float32, device=self.device) if want_hidden else None
         ops.norm_residual(x_resid, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xf, out_f32=hid,
                           row_map=logits_rows, write_resid=False)
-        logits = None
-        if want_logits:
-            logits = torch.empty(rows, w.vocab, dtype=torch.float32, device=self.device)
-            ops.gemm(xf, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
+        logits = self.lm_head(xf, rows, fresh=True) if want_logits else None
         return logits, hid
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.tp > 1:
+            self.comm.all_reduce(t)
+
+    def lm_head(self, xf: torch.Tensor, rows: int, fresh: bool = False, name: str = "lm"):
+        """Full-vocabulary logits fp32 [rows][V] from normalised bf16 rows (modeling_gemma.py:530-534).
+        Under TP each rank computes its vocabulary slice into its slot of a zeroed [rows][W][V/W]
+        buffer and a SUM all-reduce assembles the rows (exact: every other slot adds 0)."""
+        w = self.w
+        alloc = (lambda shape: torch.empty(*shape, dtype=torch.float32, device=self.device)) if fresh else \
+            (lambda shape: self._buf(name, shape, torch.float32))
+        if self.tp == 1:
+            logits = alloc((rows, w.vocab))
+            ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32, bias=w.lm_bias)
+            return logits
+        vl = w.vocab_local
+        vlp = _rup(vl, 4)                                                 # 16-byte aligned slots
+        g = alloc((rows, self.tp, vlp))
+        g.zero_()
+        ops.gemm(xf, w.lm_w, g[:, self.comm.rank, :vl], epi=ops.EPI_F32, bias=w.lm_bias, M=rows)
+        self._allreduce(g)
+        return g.view(rows, w.vocab) if vlp == vl else g[:, :, :vl].reshape(rows, w.vocab)
 
     # ------------------------------------------------------------------ decode step (graph-capturable)
     def decode_state(self, B: int, cache: KVStore, positions_next: torch.Tensor, max_steps: int):
@@ -236,14 +271,13 @@ class PaliGemmaEngine:
         xn = self._buf("d_xn", (B, H), torch.bfloat16)
         qb = self._buf("d_q", (B, nh * hd), torch.bfloat16)
         h = self._buf("d_h", (B, I), torch.bfloat16)
-        so, sd = self.DECODE_SPLIT_O, self.DECODE_SPLIT_DOWN
+        so, sd = self.split_o, self.split_down
         part = self._buf("d_part", (max(so, sd), B, H), torch.float32)
         SK = self.DECODE_SPLIT_KEYS
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
         dt = (hd + 15) // 16 * 16
         part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
         part_ml = self._buf("d_pml", (B * nkv * nsplit * 16 * 2,), torch.float32)
-        logits = self._buf("d_logits", (B, w.vocab), torch.float32)
         ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, res_a,
                         image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
                         normalizer=float(w.hidden ** 0.5))
@@ -261,13 +295,26 @@ class PaliGemmaEngine:
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv)
             ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32, M=B, ksplit=so)
+            self._allreduce(part[:so])
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=so,
                                 norm_w=Lw["post_w"], eps=1e-6)
             ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
             ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=sd)
+            self._allreduce(part[:sd])
             ns = sd
         ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
-        ops.gemm(xn, w.embed, logits, epi=ops.EPI_F32, bias=w.lm_bias)
+        if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
+            # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
+            loc = self._buf("d_logits_loc", (B, _rup(w.vocab_local, 4)), torch.float32)[:, :w.vocab_local]
+            ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32, bias=w.lm_bias)
+            pairs = self._buf("d_pairs", (self.tp, B, 2), torch.float32)
+            pairs.zero_()
+            ops.argmax_pairs(loc, st["ws"], pairs[self.comm.rank], vocab_offset=w.vocab_offset)
+            self._allreduce(pairs)
+            ops.argmax_merge(pairs, st["ids"], world=self.tp, hist=st["hist"], step=st["step"], pos=st["pos"],
+                             kv_len=st["kv_len"])
+            return loc
+        logits = self.lm_head(xn, B, name="d_logits")
         if sampler is not None:
             self.sample(logits, st, sampler, advance=True)
         return logits
@@ -313,6 +360,7 @@ class PaliGemmaEngine:
             sampler["uniforms"] = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
         self.sample(logits, st, sampler, advance=False)                  # token 1 from the prefill logits
         n = 1
+        use_graph = use_graph and self.comm.capturable
         step_fn = self._graph_step(st, cache, feats, sampler) if use_graph else \
             (lambda: self.decode_step(st, cache, feats, sampler))
         while n < max_new_tokens:

@@ -53,7 +53,7 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
     if epi == EPI_F32:
         _chk(out, torch.float32, "out")
         need = ksplit * M * ldc
-        if out.numel() < need:
+        if out.is_contiguous() and out.numel() < need or not out.is_contiguous() and ksplit > 1:
             raise ValueError("pghip.gemm: partial output too small")
     elif epi == EPI_F32_POS:
         _chk(out, torch.float32, "out")
@@ -146,6 +146,17 @@ def argmax(logits, out_ids, workspace, *, hist=None, step=None, pos=None, kv_len
     B, V = logits.shape
     _lib.call("pg_argmax", _p(logits), logits.stride(0), B, V, _p(workspace), _p(out_ids), _p(hist), _p(step),
               _p(pos), _p(kv_len), _s())
+
+
+def argmax_pairs(logits, workspace, pairs, *, vocab_offset: int):
+    _chk(logits, torch.float32, "logits")
+    B, V = logits.shape
+    _lib.call("pg_argmax_pairs", _p(logits), logits.stride(0), B, V, int(vocab_offset), _p(workspace), _p(pairs), _s())
+
+
+def argmax_merge(pairs, out_ids, *, world: int, hist=None, step=None, pos=None, kv_len=None):
+    B = out_ids.numel()
+    _lib.call("pg_argmax_merge", _p(pairs), int(world), B, _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _s())
 
 
 def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, step=None, pos=None, kv_len=None,

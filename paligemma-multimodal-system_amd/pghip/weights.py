@@ -15,6 +15,13 @@ tensors of any float dtype on any device.  Output, on the HIP device:
            down W [H][I], fp32 RMSNorm weights (the kernel applies 1 + w).
 
 Padding rows/columns are zero so padded outputs are exactly 0 (gelu(0) = 0).
+
+Tensor parallelism (tp_world > 1): rank r keeps the q heads
+[r*nh/W, (r+1)*nh/W) and every (replicated) k/v head, the matching o_proj input columns,
+the gate/up rows and down input columns of its slice [r*I/W, (r+1)*I/W) of the
+intermediate dimension, and the lm_head rows (= embedding rows) of its vocabulary slice
+[r*V/W, (r+1)*V/W).  o_proj and down then produce partial sums that one all-reduce
+completes; the embedding gather, RMSNorm weights and the vision tower stay replicated.
 """
 from __future__ import annotations
 
@@ -35,8 +42,12 @@ def rope_row_perm(D: int) -> torch.Tensor:
 
 
 class PackedWeights:
-    def __init__(self, cfg: dict, get, device="cuda", parts=("vision", "proj", "text")):
+    def __init__(self, cfg: dict, get, device="cuda", parts=("vision", "proj", "text"), tp_rank: int = 0,
+                 tp_world: int = 1):
         self.cfg = cfg
+        self.tp_rank, self.tp_world = int(tp_rank), int(tp_world)
+        if not 0 <= self.tp_rank < self.tp_world:
+            raise ValueError(f"tp_rank {tp_rank} outside tp_world {tp_world}")
         self.device = torch.device(device)
         self.parts = tuple(parts)
         v, t = cfg["vision_config"], cfg.get("text_config")
@@ -102,41 +113,55 @@ class PackedWeights:
 
     def _pack_text(self, t, get, dev, bf, f32):
         # ---------------- Gemma
+        R, W = self.tp_rank, self.tp_world
         self.hidden = t["hidden_size"]
-        self.heads = t["num_attention_heads"]
+        self.heads_total = t["num_attention_heads"]
         self.kv_heads = t["num_key_value_heads"]
         self.head_dim = t.get("head_dim", 256)
-        self.inter = t["intermediate_size"]
+        self.inter_total = t["intermediate_size"]
         self.t_layers = t["num_hidden_layers"]
         self.vocab = t["vocab_size"]
         self.rope_theta = t.get("rope_theta", 10000.0)
-        if self.inter % 16:
-            raise ValueError("intermediate_size must be a multiple of 16 for the gate/up interleave")
+        if self.heads_total % W or (self.heads_total // W) % self.kv_heads:
+            raise ValueError(f"{self.heads_total} q heads do not split over {W} ranks x {self.kv_heads} kv heads")
+        if self.inter_total % (16 * W):
+            raise ValueError("intermediate_size / tp_world must be a multiple of 16 for the gate/up interleave")
+        if self.vocab % W:
+            raise ValueError(f"vocab_size {self.vocab} does not split over {W} ranks")
         if self.head_dim % 16:
             raise ValueError("head_dim must be a multiple of 16 for the fused RoPE epilogue")
-        perm = rope_row_perm(self.head_dim).to(dev)
+        self.heads = self.heads_total // W                    # q heads held by this rank
+        self.inter = self.inter_total // W                    # intermediate slice held by this rank
+        self.vocab_local = self.vocab // W
+        self.vocab_offset = R * self.vocab_local
+        hd, H, I = self.head_dim, self.hidden, self.inter
+        q_lo, q_hi = R * self.heads * hd, (R + 1) * self.heads * hd
+        i_lo, i_hi = R * I, (R + 1) * I
+        perm = rope_row_perm(hd).to(dev)
         nblk = self.heads + 2 * self.kv_heads
         lm = "language_model."
         self.embed = bf(get(lm + "model.embed_tokens.weight"))
-        self.lm_bias = f32(get(lm + "lm_head.bias"))
-        H, I = self.hidden, self.inter
+        self.lm_w = self.embed[self.vocab_offset:self.vocab_offset + self.vocab_local]   # tied lm_head rows
+        self.lm_bias = f32(get(lm + "lm_head.bias"))[self.vocab_offset:self.vocab_offset + self.vocab_local]
+        self.lm_bias = self.lm_bias.contiguous()
         self.tl = []
         for i in range(self.t_layers):
             lp = f"{lm}model.layers.{i}."
             a = lp + "self_attn."
-            qkv_w = torch.cat([bf(get(a + "q_proj.weight")), bf(get(a + "k_proj.weight")),
+            qkv_w = torch.cat([bf(get(a + "q_proj.weight")[q_lo:q_hi]), bf(get(a + "k_proj.weight")),
                                bf(get(a + "v_proj.weight"))], 0)
-            qkv_w = qkv_w.view(nblk, self.head_dim, H)[:, perm, :].reshape(nblk * self.head_dim, H).contiguous()
-            g = bf(get(lp + "mlp.gate_proj.weight")).reshape(I // 16, 16, H)
-            u = bf(get(lp + "mlp.up_proj.weight")).reshape(I // 16, 16, H)
+            qkv_w = qkv_w.view(nblk, hd, H)[:, perm, :].reshape(nblk * hd, H).contiguous()
+            g = bf(get(lp + "mlp.gate_proj.weight")[i_lo:i_hi]).reshape(I // 16, 16, H)
+            u = bf(get(lp + "mlp.up_proj.weight")[i_lo:i_hi]).reshape(I // 16, 16, H)
             gu = torch.stack([g, u], dim=1).reshape(2 * I, H).contiguous()
             self.tl.append(dict(
-                in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=qkv_w, o_w=bf(get(a + "o_proj.weight")),
+                in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=qkv_w,
+                o_w=bf(get(a + "o_proj.weight")[:, q_lo:q_hi]),
                 post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=gu,
-                down_w=bf(get(lp + "mlp.down_proj.weight"))))
+                down_w=bf(get(lp + "mlp.down_proj.weight")[:, i_lo:i_hi])))
             del g, u
         self.final_w = f32(get(lm + "model.norm.weight"))
-        self.qkv_n = (self.heads + 2 * self.kv_heads) * self.head_dim
+        self.qkv_n = (self.heads + 2 * self.kv_heads) * hd
 
     def nbytes(self) -> int:
         n = 0
@@ -151,4 +176,4 @@ class PackedWeights:
     def decode_weight_bytes(self) -> int:
         """HBM bytes of weights one decode step streams (Gemma linears + tied lm_head)."""
         n = sum(sum(d[k].numel() * 2 for k in ("qkv_w", "o_w", "gu_w", "down_w")) for d in self.tl)
-        return n + self.embed.numel() * 2
+        return n + self.lm_w.numel() * 2

@@ -1,0 +1,85 @@
+"""Rank body of tests/test_tp_gpu.py (launched by torch.distributed.run, 2 ranks on one HIP device,
+gloo transport): the tensor-parallel engine against the reference's golden vectors and the
+single-rank engine.  Writes one JSON verdict per rank to $TP_OUT/rank<r>.json."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "paligemma-multimodal-system_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def err(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    from pghip import configs, engine, synthetic, weights
+    from pghip.tp import TPComm
+    cfg = configs.TINY
+    sd = synthetic.SyntheticStateDict(cfg)
+    tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
+                                comm=TPComm())
+    solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "tiny.npz")))
+    out = {"rank": rank, "world": world}
+    for B in (1, 2):
+        p = f"b{B}_"
+        ids = torch.from_numpy(g[p + "input_ids"]).cuda()
+        px = torch.from_numpy(g[p + "pixel_values"]).cuda()
+        Bv, L = ids.shape
+        cache = tp.new_cache(Bv, L + 8)
+        resid = torch.empty(Bv * L, tp.w.hidden, device="cuda")
+        tp.embed_merge(ids, tp.vision(px), resid)
+        pos = torch.arange(1, L + 1, dtype=torch.int32).repeat(Bv, 1)
+        logits, _ = tp.gemma_prefill(resid, pos, cache, Bv, L)
+        out[f"prefill_err_b{B}"] = err(logits.cpu().numpy(), g[p + "logits"].reshape(Bv * L, -1))
+    ids = torch.from_numpy(g["b1_input_ids"]).cuda()
+    px = torch.from_numpy(g["b1_pixel_values"]).cuda()
+    am = torch.ones_like(ids)
+    out["greedy"] = tp.generate(ids, px, am, len(g["greedy_ids"]))[0].tolist()
+    out["greedy_ref"] = g["greedy_ids"].tolist()
+    # long teacher-forced decode: TP logits (gathered full vocabulary) vs the single-rank engine
+    steps = 20
+    caches, nxts, feats = [], [], []
+    for e in (tp, solo):
+        c, f, lg, n = e.prefill_request(ids, px, am, steps)
+        caches.append(c), nxts.append(n), feats.append(f)
+    st = [e.decode_state(1, c, n, steps) for e, c, n in zip((tp, solo), caches, nxts)]
+    worst, agree = 0.0, True
+    for t in range(steps - 1):
+        tok = 7 + 13 * t
+        lgs = []
+        for e, s, c, f in zip((tp, solo), st, caches, feats):
+            s["ids"].fill_(tok)
+            lgs.append(e.decode_step(s, c, f, dict(do_sample=False)).clone())
+        if int(st[0]["ids"][0]) != int(st[1]["ids"][0]):
+            agree = False
+        # the greedy TP path returns the local vocabulary slice; compare it with the same slice
+        lo = tp.w.vocab_offset
+        worst = max(worst, err(lgs[0].cpu().numpy(), lgs[1][:, lo:lo + tp.w.vocab_local].cpu().numpy()))
+    out["decode_slice_err"] = worst
+    out["decode_argmax_agree"] = agree
+    # top-p sampling with the same uniforms through the gathered logits
+    u = torch.rand(9, 1, generator=torch.Generator().manual_seed(3))
+    out["sampled_tp"] = tp.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
+                                    stop_token=None)[0].tolist()
+    out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
+                                        stop_token=None)[0].tolist()
+    torch.cuda.synchronize()
+    with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
