@@ -175,6 +175,8 @@ def main():
 
     st = setup()
     try:
+        if not eng.comm.capturable:
+            raise RuntimeError(f"{eng.comm.backend} collectives are not graph-capturable")
         replay = eng._graph_step(st, state["cache"], state["feats"], dict(do_sample=False))
     except Exception as e:  # collectives that cannot be captured: eager decode steps
         log(f"[bench] rank {rank}: decode-step capture failed ({e}); running eager steps")

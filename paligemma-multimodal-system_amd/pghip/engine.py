@@ -233,11 +233,10 @@ class PaliGemmaEngine:
             logits = alloc((rows, w.vocab))
             ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32, bias=w.lm_bias)
             return logits
-        vl = w.vocab_local
-        vlp = _rup(vl, 4)                                                 # 16-byte aligned slots
+        vl, vlp = w.vocab_local, w.vocab_local_pad                       # 16-byte aligned slots
         g = alloc((rows, self.tp, vlp))
         g.zero_()
-        ops.gemm(xf, w.lm_w, g[:, self.comm.rank, :vl], epi=ops.EPI_F32, bias=w.lm_bias, M=rows)
+        ops.gemm(xf, w.lm_w, g[:, self.comm.rank], epi=ops.EPI_F32, bias=w.lm_bias, M=rows)  # pad rows give 0
         self._allreduce(g)
         return g.view(rows, w.vocab) if vlp == vl else g[:, :, :vl].reshape(rows, w.vocab)
 
@@ -305,8 +304,9 @@ class PaliGemmaEngine:
         ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
         if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
             # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
-            loc = self._buf("d_logits_loc", (B, _rup(w.vocab_local, 4)), torch.float32)[:, :w.vocab_local]
+            loc = self._buf("d_logits_loc", (B, w.vocab_local_pad), torch.float32)
             ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32, bias=w.lm_bias)
+            loc = loc[:, :w.vocab_local]
             pairs = self._buf("d_pairs", (self.tp, B, 2), torch.float32)
             pairs.zero_()
             ops.argmax_pairs(loc, st["ws"], pairs[self.comm.rank], vocab_offset=w.vocab_offset)

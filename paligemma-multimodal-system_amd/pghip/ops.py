@@ -52,8 +52,8 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
     if epi == EPI_F32:
         _chk(out, torch.float32, "out")
-        need = ksplit * M * ldc
-        if out.is_contiguous() and out.numel() < need or not out.is_contiguous() and ksplit > 1:
+        need = (ksplit * M - 1) * ldc + N                                # last element touched, in elements
+        if out.storage_offset() + need > out.untyped_storage().nbytes() // out.element_size():
             raise ValueError("pghip.gemm: partial output too small")
     elif epi == EPI_F32_POS:
         _chk(out, torch.float32, "out")

@@ -131,19 +131,30 @@ class PackedWeights:
         if self.head_dim % 16:
             raise ValueError("head_dim must be a multiple of 16 for the fused RoPE epilogue")
         self.heads = self.heads_total // W                    # q heads held by this rank
-        self.inter = self.inter_total // W                    # intermediate slice held by this rank
+        self.inter_real = self.inter_total // W               # intermediate slice held by this rank
+        self.inter = _rup(self.inter_real, 64)                # kernel width: zero-padded to the GEMM K step
         self.vocab_local = self.vocab // W
         self.vocab_offset = R * self.vocab_local
         hd, H, I = self.head_dim, self.hidden, self.inter
         q_lo, q_hi = R * self.heads * hd, (R + 1) * self.heads * hd
-        i_lo, i_hi = R * I, (R + 1) * I
+        Ir = self.inter_real
+        i_lo, i_hi = R * Ir, (R + 1) * Ir
         perm = rope_row_perm(hd).to(dev)
         nblk = self.heads + 2 * self.kv_heads
         lm = "language_model."
         self.embed = bf(get(lm + "model.embed_tokens.weight"))
-        self.lm_w = self.embed[self.vocab_offset:self.vocab_offset + self.vocab_local]   # tied lm_head rows
-        self.lm_bias = f32(get(lm + "lm_head.bias"))[self.vocab_offset:self.vocab_offset + self.vocab_local]
-        self.lm_bias = self.lm_bias.contiguous()
+        # tied lm_head rows of this rank's vocabulary slice (a view of the embedding when no padding is
+        # needed; the GEMM wants N % 4 == 0, so an odd-sized slice gets a zero-padded copy)
+        vo, vl = self.vocab_offset, self.vocab_local
+        self.vocab_local_pad = _rup(vl, 4)
+        bias = f32(get(lm + "lm_head.bias"))[vo:vo + vl]
+        if self.vocab_local_pad == vl:
+            self.lm_w, self.lm_bias = self.embed[vo:vo + vl], bias.contiguous()
+        else:
+            self.lm_w = torch.zeros(self.vocab_local_pad, self.hidden, dtype=torch.bfloat16, device=dev)
+            self.lm_w[:vl] = self.embed[vo:vo + vl]
+            self.lm_bias = torch.zeros(self.vocab_local_pad, dtype=torch.float32, device=dev)
+            self.lm_bias[:vl] = bias
         self.tl = []
         for i in range(self.t_layers):
             lp = f"{lm}model.layers.{i}."
@@ -151,14 +162,18 @@ class PackedWeights:
             qkv_w = torch.cat([bf(get(a + "q_proj.weight")[q_lo:q_hi]), bf(get(a + "k_proj.weight")),
                                bf(get(a + "v_proj.weight"))], 0)
             qkv_w = qkv_w.view(nblk, hd, H)[:, perm, :].reshape(nblk * hd, H).contiguous()
-            g = bf(get(lp + "mlp.gate_proj.weight")[i_lo:i_hi]).reshape(I // 16, 16, H)
-            u = bf(get(lp + "mlp.up_proj.weight")[i_lo:i_hi]).reshape(I // 16, 16, H)
-            gu = torch.stack([g, u], dim=1).reshape(2 * I, H).contiguous()
+            g = torch.zeros(I, H, dtype=torch.bfloat16, device=dev)      # padded rows: gelu(0) * 0 = 0
+            u = torch.zeros(I, H, dtype=torch.bfloat16, device=dev)
+            g[:Ir] = bf(get(lp + "mlp.gate_proj.weight")[i_lo:i_hi])
+            u[:Ir] = bf(get(lp + "mlp.up_proj.weight")[i_lo:i_hi])
+            gu = torch.stack([g.view(I // 16, 16, H), u.view(I // 16, 16, H)], dim=1).reshape(2 * I, H).contiguous()
+            down = torch.zeros(H, I, dtype=torch.bfloat16, device=dev)
+            down[:, :Ir] = bf(get(lp + "mlp.down_proj.weight")[:, i_lo:i_hi])
             self.tl.append(dict(
                 in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=qkv_w,
                 o_w=bf(get(a + "o_proj.weight")[:, q_lo:q_hi]),
                 post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=gu,
-                down_w=bf(get(lp + "mlp.down_proj.weight")[:, i_lo:i_hi])))
+                down_w=down))
             del g, u
         self.final_w = f32(get(lm + "model.norm.weight"))
         self.qkv_n = (self.heads + 2 * self.kv_heads) * hd

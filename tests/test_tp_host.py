@@ -51,7 +51,7 @@ def _worker(rank, world, port, cfg_name):
         W = synth.generate_state_dict(cfg)
         P = PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu", parts=("text",), tp_rank=rank,
                           tp_world=world)
-        assert P.heads * world == tc["num_attention_heads"] and P.inter * world == tc["intermediate_size"]
+        assert P.heads * world == tc["num_attention_heads"] and P.inter_real * world == tc["intermediate_size"]
         rng = np.random.default_rng(7)
         B, L, H = 2, 9, tc["hidden_size"]
         x = (rng.standard_normal((B, L, H)) * 0.5).astype(np.float32)
@@ -73,13 +73,13 @@ def _worker(rank, world, port, cfg_name):
             np.testing.assert_allclose(t.numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
         # vocabulary-parallel lm_head: each rank fills its slot of a zeroed buffer, SUM all-reduce gathers
         xr = x.reshape(-1, H)
-        g = torch.zeros(xr.shape[0], world, P.vocab_local)
+        g = torch.zeros(xr.shape[0], world, P.vocab_local_pad)
         g[:, rank] = torch.from_numpy(xr) @ P.lm_w.float().T + P.lm_bias
         dist.all_reduce(g)
         full = xr @ W["language_model.model.embed_tokens.weight"].T + W["language_model.lm_head.bias"]
-        np.testing.assert_allclose(g.reshape(xr.shape[0], -1).numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
+        np.testing.assert_allclose(g[:, :, :P.vocab_local].reshape(xr.shape[0], -1).numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
         # greedy merge of per-rank (max, first index) pairs == global argmax (lowest index on ties)
-        loc = g[:, rank]
+        loc = g[:, rank, :P.vocab_local]
         pairs = torch.zeros(world, xr.shape[0], 2)
         mx, ix = loc.max(-1)
         pairs[rank, :, 0], pairs[rank, :, 1] = mx, (ix + P.vocab_offset).float()
