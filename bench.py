@@ -33,6 +33,11 @@ for _p in (ROOT, PKG):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+try:
+    with open(os.path.join(ROOT, "BASELINE.json")) as _f:
+        BASELINE_METRIC = json.load(_f)["metric"]
+except Exception:  # pragma: no cover
+    BASELINE_METRIC = "image->text tokens/sec + prefill ms, PaliGemma-3B-224 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFS = 2500.0     # dense bf16 MFMA
 
@@ -124,6 +129,8 @@ def main():
     ap.add_argument("--gen-tokens", type=int, default=128)
     ap.add_argument("--parallel", default="dp", choices=["dp", "tp"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
+                    "instead of greedy, as BASELINE configs[3]")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,11 +172,17 @@ def main():
 
     # one request = prefill + T-1 graph-replayed decode steps (first token comes from the prefill)
     state = {}
+    if args.sample:
+        g = torch.Generator().manual_seed(4321)
+        sampler = dict(do_sample=True, temperature=0.8, top_p=0.9,
+                       uniforms=torch.rand(T + 1, B, generator=g).cuda())
+    else:
+        sampler = dict(do_sample=False)
 
     def setup():
         cache, feats, logits, nxt = eng.prefill_request(ids, px, mask, T)
         st = eng.decode_state(B, cache, nxt, T)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        eng.sample(logits, st, sampler, advance=False)
         state.update(cache=cache, feats=feats, st=st)
         return st
 
@@ -177,11 +190,11 @@ def main():
     try:
         if not eng.comm.capturable:
             raise RuntimeError(f"{eng.comm.backend} collectives are not graph-capturable")
-        replay = eng._graph_step(st, state["cache"], state["feats"], dict(do_sample=False))
+        replay = eng._graph_step(st, state["cache"], state["feats"], sampler)
     except Exception as e:  # collectives that cannot be captured: eager decode steps
         log(f"[bench] rank {rank}: decode-step capture failed ({e}); running eager steps")
         torch.cuda.synchronize()
-        replay = lambda: eng.decode_step(state["st"], state["cache"], state["feats"], dict(do_sample=False))  # noqa
+        replay = lambda: eng.decode_step(state["st"], state["cache"], state["feats"], sampler)  # noqa
         graph_mode = "eager"
     else:
         graph_mode = "hipgraph"
@@ -199,7 +212,7 @@ def main():
         state["st"]["kv_len"].fill_(L)
         state["st"]["step"].zero_()
         state["feats"].copy_(feats)
-        eng.sample(logits, state["st"], dict(do_sample=False), advance=False)
+        eng.sample(logits, state["st"], sampler, advance=False)
         for _ in range(T - 1):
             replay()
 
@@ -265,15 +278,19 @@ def main():
         except Exception as e:  # report, do not fail the bench
             cpu = {"value": None, "unit": "tokens/s", "cores": os.cpu_count(), "kind": "port", "sample": f"failed: {e}"}
 
+    baseline_ref = {("pt-224", 1): "BASELINE.json configs[1]", ("pt-448", 16): "BASELINE.json configs[2]"}.get(
+        (args.config, B), "not a BASELINE.json config")
+    if tp == 2 and args.sample and args.config == "pt-224":
+        baseline_ref = "BASELINE.json configs[3] (mix-224 = the pt-224 architecture)"
     if rank == 0:
         rec = {
-            "metric": "image->text tokens/s (PaliGemma-3B-224, greedy, 128 new tokens) + prefill ms",
+            "metric": BASELINE_METRIC,
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak" if tp == 1 else "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights of the "
             "PaliGemma-3B architecture, name-seeded; random 224x224 image; 8-token prompt)",
             "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
-                                   f"{T} greedy tokens (BASELINE.json configs[1])",
+                                   f"{T} {'top-p' if args.sample else 'greedy'} tokens ({baseline_ref})",
                        "global_batch": B * (world // tp), "seq_len": L + T,
                        "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}", "decode": graph_mode},
             "prefill_ms": round(prefill_ms, 3),

@@ -18,6 +18,11 @@
 // pg_attn_combine merges.
 #include "common.h"
 
+// waves per workgroup in split (decode) mode: tuning knob (scripts/tune/), 1 = one split per workgroup
+#ifndef PG_ATTN_SPLIT_WAVES
+#define PG_ATTN_SPLIT_WAVES 1
+#endif
+
 struct AttnArgs {
   const bf16_t* q; long q_rs;
   bf16_t* o; long o_rs;
@@ -58,6 +63,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int g = lane >> 4;
   const int b = blockIdx.z;
   const bool split = a.split_keys > 0;
+  const int wpg = (int)(blockDim.x >> 6);
   const int nsg = split ? (int)(gridDim.y / a.Hkv) : 1;
   const int kvh = blockIdx.y / nsg;
   const int sg = blockIdx.y % nsg;
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int r0 = split ? 0 : (blockIdx.x * (int)(blockDim.x >> 6) + wave) * 16;
   int kbeg = 0, kend = Lkv, sp = 0;
   if (split) {
-    sp = sg * 4 + wave;
+    sp = sg * wpg + wave;
     kbeg = sp * a.split_keys;
     kend = min(Lkv, kbeg + a.split_keys);
   }
@@ -186,14 +192,183 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
       }
     }
   } else {
-    const int nsplit = nsg * 4;
+    const int nsplit = nsg * wpg;
     const long base = (((long)b * a.Hkv + kvh) * nsplit + sp) * 16 + c;
+    if (!rvalid) return;                       // rows past Lq*G are never merged
     float* po = a.part_o + base * (DT * 16);
 #pragma unroll
     for (int t = 0; t < DT; ++t) *(f32x4*)(po + 16 * t + 4 * g) = o[t];
     if (g == 0) {
       a.part_ml[base * 2 + 0] = m;
       a.part_ml[base * 2 + 1] = l;
+    }
+  }
+}
+
+// LDS-staged prefill attention for long sequences / large batches: a workgroup of 4 waves (64 query
+// rows of one (b, kv head)) shares every 32-key block of K and V^T through a double-buffered LDS stage,
+// so K/V leave L2 once per 64 rows instead of once per 16 (pt-448 x16: 1 MB of K/V per 16 rows).
+// Rows are padded by 16 B so the MFMA fragment reads are bank-conflict free; K rows past Lkv are
+// clamped (their scores are masked) and V^T keys past Lkv are zeroed at staging.
+template <int DP, int DT>
+__global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
+  constexpr int KS = DP / 32;
+  constexpr int KROW = DP * 2 + 16;          // bytes per staged K row
+  constexpr int VROW = 64 + 16;              // bytes per staged V^T row (32 keys)
+  constexpr int KBYTES = 32 * KROW;
+  constexpr int STAGE = KBYTES + DT * 16 * VROW;
+  constexpr int KCH = DP / 8;                // 16-B chunks per K row
+  constexpr int KITEMS = 32 * KCH;
+  constexpr int VITEMS = DT * 16 * 4;        // 4 chunks of 8 keys per V^T row
+  constexpr int KPT = (KITEMS + 255) / 256, VPT = (VITEMS + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.z, kvh = blockIdx.y;
+  const int Lkv = (a.lkv_dev ? *a.lkv_dev : 0) + a.Lkv;
+  const int R = a.Lq * a.G;
+  const int D = a.D;
+  const int r = (blockIdx.x * 4 + wave) * 16 + c;
+  const bool rvalid = r < R;                 // invalid rows still stage and hit every barrier
+  const int pos = rvalid ? r / a.G : 0;
+  const int hq = kvh * a.G + (rvalid ? r % a.G : 0);
+
+  bf16x8 qf[KS];
+  {
+    const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int d0 = 32 * s + 8 * g;
+      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
+    }
+  }
+  const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
+  const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
+  const float* mrow = a.mask ? a.mask + (long)b * a.mask_bs + (long)pos * a.mask_rs : nullptr;
+
+  u32x4 kst[KPT], vst[VPT];
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int idx = t + i * 256;
+      if (idx < KITEMS) {
+        const int key = idx / KCH, ch = idx % KCH;
+        const int kk = min(kb + key, Lkv - 1);
+        const bool ok = ch * 8 < D;
+        kst[i] = ld16_sel(kbase + (long)kk * a.k_rs + (ok ? ch * 8 : 0), ok);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int idx = t + i * 256;
+      if (idx < VITEMS) {
+        const int d = idx >> 2, key0 = kb + 8 * (idx & 3);
+        const bool dok = d < D;
+        const u32x4 v = *(const u32x4*)(vbase + (long)(dok ? d : D - 1) * a.vt_ds + key0);
+        const int nv = dok ? Lkv - key0 : 0;  // valid keys among the 8
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = nv >= 2 * j + 2 ? v[j] : (nv == 2 * j + 1 ? (v[j] & 0xFFFFu) : 0u);
+        vst[i] = o;
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* ks = smem + buf * STAGE;
+    char* vs = ks + KBYTES;
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int idx = t + i * 256;
+      if (idx < KITEMS) *(u32x4*)(ks + (idx / KCH) * KROW + (idx % KCH) * 16) = kst[i];
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int idx = t + i * 256;
+      if (idx < VITEMS) *(u32x4*)(vs + (idx >> 2) * VROW + (idx & 3) * 16) = vst[i];
+    }
+  };
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) o[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const float LOG2E = 1.4426950408889634f;
+  const int nblk = (Lkv + 31) / 32;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ib = 0; ib < nblk; ++ib) {
+    const int kb = ib * 32;
+    const int cur = ib & 1;
+    if (ib + 1 < nblk) gload(kb + 32);        // next block in flight during this block's math
+    const char* ks = smem + cur * STAGE;
+    const char* vs = ks + KBYTES;
+    f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 ka = *(const bf16x8*)(ks + c * KROW + (32 * s + 8 * g) * 2);
+      const bf16x8 kb2 = *(const bf16x8*)(ks + (16 + c) * KROW + (32 * s + 8 * g) * 2);
+      sA = mfma16(ka, qf[s], sA);
+      sB = mfma16(kb2, qf[s], sB);
+    }
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k0 = kb + 4 * g + j, k1 = kb + 16 + 4 * g + j;
+      float v0 = sA[j] * a.scale_log2, v1 = sB[j] * a.scale_log2;
+      if (mrow) {
+        v0 += mrow[min(k0, Lkv - 1)] * LOG2E;
+        v1 += mrow[min(k1, Lkv - 1)] * LOG2E;
+      }
+      x[j] = k0 < Lkv ? v0 : -INFINITY;
+      x[4 + j] = k1 < Lkv ? v1 : -INFINITY;
+    }
+    float bm = x[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { x[j] = exp2f(x[j] - mn); rs += x[j]; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+    u32x4 pw;
+    pw[0] = pack_bf2(x[0], x[1]);
+    pw[1] = pack_bf2(x[2], x[3]);
+    pw[2] = pack_bf2(x[4], x[5]);
+    pw[3] = pack_bf2(x[6], x[7]);
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+    for (int tt = 0; tt < DT; ++tt) {
+      const char* vr = vs + (16 * tt + c) * VROW;
+      const u32x2 v0 = *(const u32x2*)(vr + 8 * g);
+      const u32x2 v1 = *(const u32x2*)(vr + 32 + 8 * g);
+      o[tt] = mfma16(__builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]}), pf, o[tt] * alpha);
+    }
+    if (ib + 1 < nblk) {
+      lstore(cur ^ 1);                         // buffer cur^1 was last read before the previous barrier
+      __syncthreads();
+    }
+  }
+  if (!rvalid) return;
+  const float inv = 1.0f / l;
+  bf16_t* op = a.o + ((long)b * a.Lq + pos) * a.o_rs + (long)hq * D;
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) {
+    const int d = 16 * tt + 4 * g;
+    if (d < D) {
+      u32x2 p;
+      p[0] = pack_bf2(o[tt][0] * inv, o[tt][1] * inv);
+      p[1] = pack_bf2(o[tt][2] * inv, o[tt][3] * inv);
+      *(u32x2*)(op + d) = p;
     }
   }
 }
@@ -241,7 +416,11 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 
 #define ATTN_DISPATCH(DP_, DT_)                                                             \
   if (DP == DP_ && DT == DT_) {                                                              \
-    hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(split_keys > 0 ? 256 : 64), 0, stream, a); \
+    if (use_lds)                                                                             \
+      hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
+    else                                                                                     \
+      hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(split_keys > 0 ? 64 * PG_ATTN_SPLIT_WAVES : 64), 0, \
+                         stream, a);                                                         \
     launched = true;                                                                         \
   }
 
@@ -264,9 +443,16 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
              (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, mask, mask_bs, mask_rs,
              Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml};
   dim3 grid;
-  if (split_keys > 0) {
+  // prefill with >= 1024 one-wave workgroups: the LDS-staged kernel (64 rows per workgroup share K/V);
+  // needs 16-B aligned V^T rows / batch offsets
+  const long wgs16 = (long)((Lq * G + 15) / 16) * Hkv * B;
+  const bool use_lds = split_keys == 0 && wgs16 >= 1024 && vt_ds % 8 == 0 && vt_bs % 8 == 0 && vt_hs % 8 == 0 &&
+                       k_rs % 8 == 0 && k_bs % 8 == 0 && k_hs % 8 == 0 && q_rs % 8 == 0;
+  if (use_lds) {
+    grid = dim3((Lq * G + 63) / 64, Hkv, B);
+  } else if (split_keys > 0) {
     PG_REQUIRE(Lq * G <= 16 && nsplit % 4 == 0 && part_o && part_ml && split_keys % 32 == 0);
-    grid = dim3(1, Hkv * (nsplit / 4), B);
+    grid = dim3(1, Hkv * (nsplit / PG_ATTN_SPLIT_WAVES), B);
   } else {
     grid = dim3((Lq * G + 15) / 16, Hkv, B);   // one wave (16 query rows) per workgroup: 4x the workgroups
   }

@@ -347,6 +347,15 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 // For PRO != 0 the WG's K range of x is built in LDS (bf16, rows padded by 16 B against bank conflicts).
 #define XPAD 8
 
+// tuning knobs (scripts/tune/): issue the first weight chunks before the prologue; one-pass online
+// merge of the split-KV partials in the attention-merge prologue
+#ifndef PG_GEMV_PREW
+#define PG_GEMV_PREW 1
+#endif
+#ifndef PG_MERGE_V2
+#define PG_MERGE_V2 1
+#endif
+
 template <int PRO>
 __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, int k0, int Kr, bf16_t* xs,
                                               float* scratch) {
@@ -360,13 +369,14 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
     float* red = scratch;   // [4 waves][16 rows]
     if (M == 1 && K4 <= 4 * 256) {
       // one row: keep it in registers between the two passes (one dependent round trip fewer)
-      f32x4 v[4];
+      f32x4 v[4], wn[4];
       float ss = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int c = t + i * 256;
         v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
         if (c < K4) {
+          wn[i] = ((const f32x4*)f.norm_w)[c];          // issued with the residual: one round trip
           f32x4 a = ((const f32x4*)f.resid_in)[c];
           for (int sp = 0; sp < f.nsplit; ++sp) a += ((const f32x4*)(f.partials + (size_t)sp * K))[c];
           v[i] = a;
@@ -382,7 +392,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
       for (int i = 0; i < 4; ++i) {
         const int c = t + i * 256;
         if (c < K4) {
-          const f32x4 w = ((const f32x4*)f.norm_w)[c];
+          const f32x4 w = wn[i];
           u32x2 pk;
           pk[0] = pack_bf2((v[i][0] * rstd) * (1.0f + w[0]), (v[i][1] * rstd) * (1.0f + w[1]));
           pk[1] = pack_bf2((v[i][2] * rstd) * (1.0f + w[2]), (v[i][3] * rstd) * (1.0f + w[3]));
@@ -415,6 +425,35 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         pk[1] = pack_bf2((v[2] * rstd) * (1.0f + w[2]), (v[3] * rstd) * (1.0f + w[3]));
         *(u32x2*)(xs + m * ldx + c * 4) = pk;
       }
+    }
+  } else if constexpr (PRO == 2 && PG_MERGE_V2) {
+    // one pass per (row, head, 4 dims): online merge over the splits, no LDS staging / barriers
+    const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
+    const int h0 = k0 / D, nh = Kr / D, D4 = D >> 2;
+    const int items = M * nh * D4;
+    for (int idx = t; idx < items; idx += 256) {
+      const int m = idx / (nh * D4), rem = idx % (nh * D4), hl = rem / D4, d4 = rem % D4;
+      const int hq = h0 + hl;
+      const long base0 = (((long)m * f.kv_heads + hq / G) * S) * 16 + (hq % G);
+      float mx = -INFINITY, den = 0.f;
+      f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+      for (int sp = 0; sp < S; ++sp) {
+        const long bs = base0 + (long)sp * 16;
+        const float ms = f.part_ml[bs * 2], ls = f.part_ml[bs * 2 + 1];
+        const f32x4 o4 = *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+        const float mn = fmaxf(mx, ms);
+        const float ca = mx == -INFINITY ? 0.f : exp2f(mx - mn);
+        const float cb = ms == -INFINITY ? 0.f : exp2f(ms - mn);
+        den = den * ca + cb * ls;
+        num = num * ca + cb * o4;
+        mx = mn;
+      }
+      const float inv = 1.0f / den;
+      u32x2 pk;
+      pk[0] = pack_bf2(num[0] * inv, num[1] * inv);
+      pk[1] = pack_bf2(num[2] * inv, num[3] * inv);
+      *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
     }
   } else if constexpr (PRO == 2) {
     // x[m][k], k = hq*D + d over this WG's K range; partial row of q head hq: (kvh = hq / G, row = hq % G)
@@ -515,8 +554,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  // (issuing the first weight chunks before the prologue measured no gain: the prologue's in-order
-  //  vmcnt waits drain them anyway)
+  if constexpr (PRO != 0 && PG_GEMV_PREW) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+      if (d < mine) loadw(d, wb[d]);
+  }
   if constexpr (PRO != 0) {
     float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
     gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch);
@@ -524,7 +566,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
     if (d < mine) {
-      loadw(d, wb[d]);
+      if (!(PRO != 0 && PG_GEMV_PREW)) loadw(d, wb[d]);
       loadx(d, xb[d]);
     }
   for (int base = 0; base < mine; base += DEPTH) {

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpghip.so")
+# PGHIP_LIB selects a tuning build of the same sources (scripts/tune/); default: the in-tree product build
+LIB_PATH = os.environ.get("PGHIP_LIB") or os.path.join(_HERE, "libpghip.so")
 
 vp, i32, i64, f32, u32 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint
 

@@ -39,32 +39,35 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+def _compile(src: str, obj_dir: str = OBJ_DIR, defines=()) -> str:
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=()) -> str:
+    """Build the library.  `out`/`defines` make a tuning variant (e.g. scripts/tune/*.so with -DPG_...=1);
+    the product library is always the default build at pghip/libpghip.so."""
+    if out == LIB and not defines and not force and not _stale():
         return LIB
-    os.makedirs(OBJ_DIR, exist_ok=True)
+    obj_dir = OBJ_DIR if out == LIB else os.path.join(OBJ_DIR, os.path.basename(out).replace(".so", ""))
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(_compile, srcs))
-    tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines), srcs))
+    tmp = out + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     if verbose:
-        print(f"[pghip] built {LIB} from {len(srcs)} sources for {ARCH}")
-    return LIB
+        print(f"[pghip] built {out} from {len(srcs)} sources for {ARCH}" + (f" {list(defines)}" if defines else ""))
+    return out
 
 
 if __name__ == "__main__":

@@ -65,6 +65,7 @@ class PaliGemmaEngine:
     DECODE_SPLIT_O = 2      # split-K of o_proj at decode (partials reduced by the next RMSNorm)
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
+    FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -281,7 +282,10 @@ class PaliGemmaEngine:
                         image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
                         normalizer=float(w.hidden ** 0.5))
         ns = 0
-        for i, Lw in enumerate(w.tl):
+        if B > self.FUSE_MAX_B:
+            ns = self._decode_layers_unfused(st, cache, res_a, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t,
+                                             sin_t)
+        for i, Lw in enumerate(w.tl if B <= self.FUSE_MAX_B else ()):
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
                                 norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
                                 rows_per_batch=1, slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i],
@@ -318,6 +322,37 @@ class PaliGemmaEngine:
         if sampler is not None:
             self.sample(logits, st, sampler, advance=True)
         return logits
+
+    def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
+        """Decode layers for B > FUSE_MAX_B: the RMSNorm and the split-KV merge run once as their own
+        kernels (fused into every GEMV workgroup they would be recomputed B-fold per workgroup)."""
+        w = self.w
+        B = st["ids"].numel()
+        nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
+        kvd = nkv * hd
+        so, sd = self.split_o, self.split_down
+        attn = self._buf("d_attn", (B, nh * hd), torch.bfloat16)
+        ns = 0
+        for i, Lw in enumerate(w.tl):
+            ops.norm_residual(res, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
+                                slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
+                                q_heads=nh, kv_heads=nkv)
+            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                          scale=1.0 / math.sqrt(hd), split_keys=self.DECODE_SPLIT_KEYS, nsplit=nsplit, part_o=part_o,
+                          part_ml=part_ml)
+            ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=so)
+            self._allreduce(part[:so])
+            ops.norm_residual(res, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=so, out=xn)
+            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=sd)
+            self._allreduce(part[:sd])
+            ns = sd
+        return ns
 
     def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool):
         kw = dict(hist=st["hist"], step=st["step"])

@@ -1,0 +1,6 @@
+# pt-448 batch 16 (BASELINE configs[2]) bench line + PMC traffic pass on the pt-224 bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 600 python bench.py --config pt-448 --batch 16 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/b448.json 2> gpurun_out/b448.err || { tail -30 gpurun_out/b448.err; exit 1; }
+cat gpurun_out/b448.json

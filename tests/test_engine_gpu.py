@@ -63,10 +63,13 @@ def test_tiny_greedy_matches_reference_loop(tiny, golden):
         assert out[0].tolist() == g["greedy_ids"].tolist()
 
 
-def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden):
-    """Long decode (no EOS stop) with the oracle's greedy continuation: per-step logits."""
+@pytest.mark.parametrize("fuse_max_b", [2, 0])
+def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b):
+    """Long decode (no EOS stop) with the oracle's greedy continuation: per-step logits.  fuse_max_b=0
+    forces the unfused decode layer (separate RMSNorm / split-KV merge kernels, the B > 2 path)."""
     from oracle import paligemma_oracle as O
     eng, orc = tiny
+    eng.FUSE_MAX_B = fuse_max_b
     g = golden("tiny")
     ids_np = g["b1_input_ids"]
     steps = 24
@@ -84,6 +87,7 @@ def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden):
         top = np.sort(ref_logits[t][0])[::-1]
         if top[0] - top[1] > 0.1:
             assert int(st["ids"][0]) == ref_ids[t], t
+    eng.FUSE_MAX_B = type(eng).FUSE_MAX_B
 
 
 @pytest.mark.slow

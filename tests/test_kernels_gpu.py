@@ -129,9 +129,11 @@ def _attn_ref(q, k, v, scale, mask=None):
     return torch.softmax(s, -1) @ v.float()
 
 
-@pytest.mark.parametrize("B,N,nh,hd", [(1, 256, 16, 72), (2, 16, 8, 24), (1, 100, 4, 64)])
+@pytest.mark.parametrize("B,N,nh,hd", [(1, 256, 16, 72), (2, 16, 8, 24), (1, 100, 4, 64),
+                                       (4, 256, 16, 72), (10, 104, 16, 72)])   # last two: LDS-staged kernel
 def test_attention_vision_layout(B, N, nh, hd):
-    """SigLIP: q/k from the fused QKV buffer, V^T from the transposed side buffer."""
+    """SigLIP: q/k from the fused QKV buffer, V^T from the transposed side buffer.  Large batches take
+    the LDS-staged kernel (>= 1024 sixteen-row groups), including a ragged last key block (N=104)."""
     from pghip import ops
     hv = nh * hd
     M = B * N
@@ -147,7 +149,8 @@ def test_attention_vision_layout(B, N, nh, hd):
 
 
 @pytest.mark.parametrize("B,L,nh,nkv,hd,masked", [(1, 264, 8, 1, 256, False), (2, 24, 4, 1, 32, True),
-                                                  (1, 70, 8, 2, 64, False)])
+                                                  (1, 70, 8, 2, 64, False),
+                                                  (8, 300, 8, 1, 256, False), (16, 130, 8, 1, 256, True)])
 def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode."""
     from pghip import ops
