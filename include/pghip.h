@@ -32,14 +32,21 @@ enum {
   PG_EPI_F32 = 3,           /* C f32 [ksplit][M][ldc] partial slabs (+bias on slab 0)          */
   PG_EPI_F32_POS = 4,       /* C f32 = acc + bias + aux[(m % aux_rows)*ldc + n]   patch+pos emb  */
   PG_EPI_BF16_VT = 5,       /* cols < aux_n -> C bf16; cols >= aux_n -> aux_out[(n-aux_n)*aux_ld + m] */
-  PG_EPI_QKV_ROPE = 6       /* fused q|k|v (rope-permuted W rows): RoPE(q) -> C, RoPE(k) -> K cache, v -> V^T
+  PG_EPI_QKV_ROPE = 6,      /* fused q|k|v (rope-permuted W rows): RoPE(q) -> C, RoPE(k) -> K cache, v -> V^T
                                cache (gemma.py:274-302 + KVCache.update :18-57); pg_gemm_fused only          */
+  PG_EPI_F32_FIN = 7        /* M <= 4: F32 slabs, then the last split of each 16-column tile adds them into
+                               fin_resid and writes ss_out (the residual add of gemma.py:401,416 + the next
+                               RMSNorm's sum of squares); pg_gemm_fused only                                  */
 };
 
 /* Fused-operation arguments of pg_gemm_fused (M <= 16 for the prologues). */
 typedef struct PgFusedArgs {
   int pro_mode;             /* 0: x = A ; 1: x = RMSNorm(resid_in + sum partials)*(1+norm_w) (gemma.py:172-181) ;
-                               2: x = merge of split-KV attention partials (pg_attn_combine folded in)      */
+                               2: x = merge of split-KV attention partials (pg_attn_combine folded in) ;
+                               3: x = resid_in*(1+norm_w), rstd from ss_in applied to the outputs (RMSNorm of a
+                                  residual finalised by a PG_EPI_F32_FIN producer) ;
+                               4: x = A (the producer's fin_x = bf16(resid*(1+norm_w))), rstd from ss_in applied
+                                  to the outputs (M <= 2)                                                     */
   const float* resid_in;
   float* resid_out;         /* written once: resid_in + sum partials (ping-pong residual stream; may be NULL) */
   const float* partials;    /* [nsplit][M][K] */
@@ -59,6 +66,12 @@ typedef struct PgFusedArgs {
   void* vtc;                /* bf16 [B][kv_heads*head_dim][smax] */
   int smax;
   int q_heads;
+  int* fin_cnt;             /* PG_EPI_F32_FIN: per-output-tile arrival tickets, zero-initialised, self-resetting */
+  float* fin_resid;         /* PG_EPI_F32_FIN: residual [M][N] the split-K slabs are added into              */
+  float* ss_out;            /* PG_EPI_F32_FIN: per-16-column-tile sum of squares [M][ss_ld]                   */
+  const float* ss_in;       /* pro_mode 3: producer's per-tile sums of squares [M][ss_ld], ss_n tiles          */
+  int ss_ld, ss_n;
+  void* fin_x;              /* PG_EPI_F32_FIN (optional): bf16 [M][N] x' = resid*(1+norm_w) for a pro_mode 4 consumer */
 } PgFusedArgs;
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,

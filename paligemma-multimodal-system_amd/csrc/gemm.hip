@@ -29,6 +29,9 @@ enum {
   PG_EPI_BF16_VT = 5,       // n < aux_n: C bf16 = acc + bias ; n >= aux_n: aux_out bf16 [(n-aux_n)][m] (ld aux_ld)
   PG_EPI_QKV_ROPE = 6,      // fused q|k|v projection (rope-permuted W rows): RoPE on q -> C, RoPE on k -> K cache,
                             // v -> V^T cache (GemmaAttention.forward :274-302 + KVCache.update)
+  PG_EPI_F32_FIN = 7,       // GEMV (M <= 16) split-K slabs as PG_EPI_F32, then the last-arriving split of each
+                            // output tile adds the slabs into fin_resid and writes the tile's sum of squares
+                            // (ss_out): the residual add + RMSNorm statistics of the NEXT norm, done in-kernel
 };
 
 // Extra arguments of the fused entry point pg_gemm_fused (mirrors PgFusedArgs in include/pghip.h).
@@ -56,6 +59,15 @@ struct PgFusedArgs {
   bf16_t* vtc;               // [B][Hkv*D][Smax]
   int smax;
   int q_heads;
+  // in-kernel split-K finalisation (PG_EPI_F32_FIN) and the prologue that consumes it (pro_mode 3:
+  // x = resid_in * (1 + norm_w), rstd from ss_in applied to the accumulators: W.(x*rstd) = rstd*(W.x))
+  int* fin_cnt;              // [gridDim.x] arrival tickets, zero between launches (the last arriver resets)
+  float* fin_resid;          // [M][N] residual the slabs are added into
+  float* ss_out;             // [M][ss_ld] per-tile sum of squares of the finalised residual
+  const float* ss_in;        // [M][ss_ld] (consumer side), ss_n tiles per row
+  int ss_ld, ss_n;
+  bf16_t* fin_x;             // PG_EPI_F32_FIN (optional): x' = bf16(resid * (1 + norm_w)) [M][N] for a pro_mode 4
+                             // consumer (x' read like A, rstd from ss_in applied to its outputs)
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -352,6 +364,12 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #ifndef PG_GEMV_PREW
 #define PG_GEMV_PREW 1
 #endif
+#ifndef PG_GEMV_NT
+#define PG_GEMV_NT 0
+#endif
+#ifndef PG_TIMING_NOPRO
+#define PG_TIMING_NOPRO 0
+#endif
 #ifndef PG_MERGE_V2
 #define PG_MERGE_V2 1
 #endif
@@ -426,6 +444,27 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         *(u32x2*)(xs + m * ldx + c * 4) = pk;
       }
     }
+  } else if constexpr (PRO == 3) {
+    // x = resid * (1 + w) over the full row (the residual was finalised by the producer's FIN epilogue);
+    // per-row rstd from the producer's per-tile sums of squares, applied in the epilogue (scratch[64 + m])
+    const int K4 = K >> 2;
+    float* red = scratch;   // [4 waves][16 rows], then rstd [16] at +64
+    for (int m = 0; m < M; ++m) {
+      for (int c = t; c < K4; c += 256) {
+        const f32x4 v = ((const f32x4*)(f.resid_in + (size_t)m * K))[c];
+        const f32x4 w = ((const f32x4*)f.norm_w)[c];
+        u32x2 pk;
+        pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
+        pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
+        *(u32x2*)(xs + m * ldx + c * 4) = pk;
+      }
+      float ssum = 0.f;
+      for (int i = t; i < f.ss_n; i += 256) ssum += f.ss_in[(size_t)m * f.ss_ld + i];
+      ssum = wave_sum(ssum);
+      if ((t & 63) == 0) red[(t >> 6) * 16 + m] = ssum;
+    }
+    __syncthreads();
+    if (t < M) red[64 + t] = rsqrtf((red[t] + red[16 + t] + red[32 + t] + red[48 + t]) / (float)K + f.eps);
   } else if constexpr (PRO == 2 && PG_MERGE_V2) {
     // one pass per (row, head, 4 dims): online merge over the splits, no LDS staging / barriers
     const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
@@ -531,7 +570,22 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 
   bf16_t* xs = (bf16_t*)dyn_smem;
   const int Kr = per_z * CH;                    // K range of this split (LDS row length)
-  const bf16_t* xrow = PRO == 0 ? A + (size_t)(xvalid ? r : 0) * lda : nullptr;
+  const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : 0) * lda : nullptr;
+  // PRO 4 (M <= 2): wave 0 loads the producer's per-tile sums of squares before the weight stream (all
+  // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
+  float ssv[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (PRO == 4) {
+    if (wave == 0) {
+      const int lpr = M == 1 ? 64 : 32;
+      const int rr = min(lane / lpr, M - 1);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = lane % lpr + k * lpr;
+        const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
+        ssv[k] = i < e.f.ss_n ? v : 0.f;
+      }
+    }
+  }
   const bf16_t* xlds = xs + (xvalid ? r : 0) * (Kr + XPAD);
 
   u32x4 wb[DEPTH][NT][U];
@@ -541,11 +595,17 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < U; ++s) wv[t][s] = *(const u32x4*)(wrow[t] + off + 8 * s);
+      for (int s = 0; s < U; ++s) {
+#if PG_GEMV_NT
+        wv[t][s] = __builtin_nontemporal_load((const u32x4*)(wrow[t] + off + 8 * s));
+#else
+        wv[t][s] = *(const u32x4*)(wrow[t] + off + 8 * s);
+#endif
+      }
   };
   auto loadx = [&](int j, u32x4 (&xv)[U]) {
     const int koff = (wave + j * 4) * CH + g * 8 * U;     // offset inside this split
-    if constexpr (PRO == 0) {
+    if constexpr (PRO == 0 || PRO == 4) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
         xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
@@ -554,19 +614,20 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  if constexpr (PRO != 0 && PG_GEMV_PREW) {
+  constexpr bool STAGED = PRO != 0 && PRO != 4;   // x built in LDS by a prologue
+  if constexpr (STAGED && PG_GEMV_PREW) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
       if (d < mine) loadw(d, wb[d]);
   }
-  if constexpr (PRO != 0) {
+  if constexpr (STAGED) {
     float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
     gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch);
   }
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
     if (d < mine) {
-      if (!(PRO != 0 && PG_GEMV_PREW)) loadw(d, wb[d]);
+      if (!(STAGED && PG_GEMV_PREW)) loadw(d, wb[d]);
       loadx(d, xb[d]);
     }
   for (int base = 0; base < mine; base += DEPTH) {
@@ -598,6 +659,87 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   // lane holds C[m = lane&15][n = tile*16 + 4*(lane>>4) + 0..3]
   const int m = r;
   const int q = 4 * g;
+  if constexpr (PRO == 3) {
+    const float* scratch = (const float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
+    const float rs = scratch[64 + (m < M ? m : 0)];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] *= rs;
+  }
+  if constexpr (PRO == 4) {
+    const int lpr = M == 1 ? 64 : 32;
+    float ss = ssv[0] + ssv[1] + ssv[2] + ssv[3];
+    for (int o = 1; o < lpr; o <<= 1) ss += __shfl_xor(ss, o, 64);
+    ss = __shfl(ss, (m < M ? m : 0) * lpr, 64);
+    const float rs = rsqrtf(ss / (float)K + e.f.eps);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] *= rs;
+  }
+  if constexpr (EPI == PG_EPI_F32_FIN) {
+    // 1. this split's slab; 2. release + ticket; 3. the last split of the tile reduces the slabs into the
+    //    residual rows it owns and writes their sum of squares (MI355X guide: in-launch split-K reduction)
+    // Slab stores are write-through (agent-scope relaxed 8-B atomic stores = global_store sc1), drained,
+    // then one relaxed agent ticket: no release fence (an L2 write-back per workgroup cost 2x the kernel).
+    // The reducer reads the slabs with sc1 loads (bypass its L1/L2), so no acquire fence either.
+    const PgFusedArgs& f = e.f;
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n0 = (tile0 + t) * 16 + q;
+      if (m < M && n0 < e.N) {
+        f32x4 v = acc[t];
+        if (e.bias && z == 0) v += load4_guard(e.bias, n0, e.N);
+        gu64* dst = (gu64*)((float*)e.C + ((size_t)z * M + m) * e.ldc + n0);
+        __hip_atomic_store(dst, __builtin_bit_cast(unsigned long long, u32x2{__float_as_uint(v[0]),
+                           __float_as_uint(v[1])}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dst + 1, __builtin_bit_cast(unsigned long long, u32x2{__float_as_uint(v[2]),
+                           __float_as_uint(v[3])}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(f.fin_cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, 0, 64);
+    if (old != (int)gridDim.y - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep the loads below the ticket
+    float ssl = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n0 = (tile0 + t) * 16 + q;
+      if (m < M && n0 < e.N) {
+        float* rp = f.fin_resid + (size_t)m * e.N + n0;
+        f32x4 v = *(const f32x4*)rp;
+        // all (<= 8) slabs in flight at once: clamped addresses + selects, no per-split branch / wait
+        const int Z = (int)gridDim.y;
+        u32x2 sa[8], sb[8];
+#pragma unroll
+        for (int zz = 0; zz < 8; ++zz) {
+          gu64* src = (gu64*)((float*)e.C + ((size_t)(zz < Z ? zz : Z - 1) * M + m) * e.ldc + n0);
+          sa[zz] = __builtin_bit_cast(u32x2, __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          sb[zz] = __builtin_bit_cast(u32x2, __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+#pragma unroll
+        for (int zz = 0; zz < 8; ++zz) {
+          const f32x4 sv = {__uint_as_float(sa[zz][0]), __uint_as_float(sa[zz][1]), __uint_as_float(sb[zz][0]),
+                            __uint_as_float(sb[zz][1])};
+          v += zz < Z ? sv : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        *(f32x4*)rp = v;
+        ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+        if (f.fin_x) {
+          const f32x4 w = *(const f32x4*)(f.norm_w + n0);
+          u32x2 pk;
+          pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
+          pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
+          *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
+        }
+      }
+    }
+    ssl += __shfl_xor(ssl, 16, 64);
+    ssl += __shfl_xor(ssl, 32, 64);
+    if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + blockIdx.x] = ssl;
+    if (lane == 0) __hip_atomic_store(f.fin_cnt + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
     epi_gelu_mul4(e, m, tile0 * 16, q, acc[0], acc[1]);
   } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
@@ -642,10 +784,11 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   const int CH = 64;                                   // U = 2
   const int per_z = (K / CH + ksplit - 1) / ksplit;
   size_t lds = 0;
-  if (PRO != 0) {
+  if (PRO != 0 && PRO != 4) {
     lds = (size_t)e.M * (per_z * CH + XPAD) * 2;
     lds = (lds + 15) & ~(size_t)15;
     if (PRO == 1) lds += 64 * sizeof(float);
+    if (PRO == 3) lds += 80 * sizeof(float);
     if (PRO == 2) {
       const int pairs = e.M * (per_z * CH / e.f.head_dim);
       lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
@@ -663,9 +806,18 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
 template <int EPI>
 static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
+#if PG_TIMING_NOPRO   // timing experiment only (wrong numerics): the fused prologues replaced by a plain x read
+  if (e.f.pro_mode != 0) {
+    const bf16_t* xa = (const bf16_t*)(e.f.pro_mode == 1 ? (const void*)e.f.resid_in : (const void*)e.f.part_o);
+    launch_gemv_pro<EPI, 0>(xa, K, W, ldw, K, ksplit, e, st);
+    return;
+  }
+#endif
   switch (e.f.pro_mode) {
     case 1: launch_gemv_pro<EPI, 1>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 2: launch_gemv_pro<EPI, 2>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 3: launch_gemv_pro<EPI, 3>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 4: launch_gemv_pro<EPI, 4>(A, lda, W, ldw, K, ksplit, e, st); break;
     default: launch_gemv_pro<EPI, 0>(A, lda, W, ldw, K, ksplit, e, st); break;
   }
 }
@@ -678,7 +830,9 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
-  if (f.pro_mode == 0) PG_REQUIRE(A != nullptr && lda >= K);
+  if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
+  if (f.pro_mode == 4) PG_REQUIRE(M <= 2 && ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_n <= 256 &&
+                                  (M == 1 || f.ss_n <= 128) && f.ss_ld >= f.ss_n);
   if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
   if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
   if (f.pro_mode == 2) PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 &&
@@ -686,7 +840,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (epi == PG_EPI_QKV_ROPE) PG_REQUIRE(f.head_dim % 16 == 0 && f.cos_t && f.sin_t && f.pos && f.kc && f.vtc &&
                                          f.rows_per_batch > 0 && f.smax > 0 && ksplit == 1 &&
                                          N == (f.q_heads + 2 * f.kv_heads) * f.head_dim);
-  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32);
+  if (f.pro_mode == 3) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && f.ss_in && f.ss_n > 0 &&
+                                  f.ss_ld >= f.ss_n && K % 4 == 0);
+  if (epi == PG_EPI_F32_FIN) PG_REQUIRE(M <= 4 && ksplit <= 8 && (f.fin_x == nullptr || f.norm_w != nullptr) && f.fin_cnt && f.fin_resid && f.ss_out && f.ss_ld >= (N + 15) / 16 &&
+                                        ldc == N);
+  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
   if (epi == PG_EPI_BF16_VT) PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
@@ -702,6 +860,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
       case PG_EPI_F32_POS: launch_gemv<PG_EPI_F32_POS>(a, lda, w, ldw, K, ksplit, e, stream); break;
       case PG_EPI_BF16_VT: launch_gemv<PG_EPI_BF16_VT>(a, lda, w, ldw, K, ksplit, e, stream); break;
       case PG_EPI_QKV_ROPE: launch_gemv<PG_EPI_QKV_ROPE>(a, lda, w, ldw, K, ksplit, e, stream); break;
+      case PG_EPI_F32_FIN: launch_gemv<PG_EPI_F32_FIN>(a, lda, w, ldw, K, ksplit, e, stream); break;
       default: return (int)hipErrorInvalidValue;
     }
   } else {

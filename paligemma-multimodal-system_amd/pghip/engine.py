@@ -66,6 +66,7 @@ class PaliGemmaEngine:
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
+    USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -285,6 +286,16 @@ class PaliGemmaEngine:
         if B > self.FUSE_MAX_B:
             ns = self._decode_layers_unfused(st, cache, res_a, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t,
                                              sin_t)
+        if B <= self.FUSE_MAX_B and self.tp == 1 and self.USE_FIN:
+            xq, ss, tiles = self._decode_layers_fin(st, cache, res_a, qb, h, part, part_o, part_ml, nsplit, dt,
+                                                    cos_t, sin_t)
+            # final RMSNorm folded into the lm_head GEMV: x' = resid*(1+w) from the last down_proj, rstd on the outputs
+            logits = self._buf("d_logits", (B, w.vocab), torch.float32)
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+            ops.gemm_fused(xq, w.lm_w, logits, fa, epi=ops.EPI_F32, M=B, bias=w.lm_bias)
+            if sampler is not None:
+                self.sample(logits, st, sampler, advance=True)
+            return logits
         for i, Lw in enumerate(w.tl if B <= self.FUSE_MAX_B else ()):
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
                                 norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
@@ -322,6 +333,59 @@ class PaliGemmaEngine:
         if sampler is not None:
             self.sample(logits, st, sampler, advance=True)
         return logits
+
+    def _zeros(self, name, shape, dtype):
+        """Persistent zero-initialised buffer (e.g. self-resetting arrival tickets)."""
+        t = self._ws.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype:
+            t = torch.zeros(*shape, dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t
+
+    def _decode_layers_fin(self, st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
+        """Decode layers (single rank, B <= FUSE_MAX_B) in 5 launches with in-kernel split-K finalisation:
+        o_proj and down_proj add their split-K slabs into the residual in place (the last-arriving split of
+        each 16-column tile), and write x' = bf16(resid*(1+w_next)) plus per-tile sums of squares; the next
+        GEMV (gate/up, the next layer's qkv, finally the lm_head) reads x' like a plain activation and
+        scales its outputs by rstd (RMSNorm: W.(x*rstd*(1+w)) = rstd * W.(x*(1+w))).
+        Returns (x', sums of squares, tiles) of the final norm for the lm_head."""
+        w = self.w
+        B = st["ids"].numel()
+        H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
+        kvd = nkv * hd
+        so, sd = self.split_o, self.split_down
+        tiles = (H + 15) // 16
+        cnt = self._zeros("d_fin_cnt", (tiles,), torch.int32)
+        ss_o = self._buf("d_ss_o", (B, tiles), torch.float32)
+        ss_d = self._buf("d_ss_d", (B, tiles), torch.float32)
+        xq = self._buf("d_xq", (B, H), torch.bfloat16)
+        SK = self.DECODE_SPLIT_KEYS
+        nl = len(w.tl)
+        for i, Lw in enumerate(w.tl):
+            rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
+                        slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
+                        q_heads=nh, kv_heads=nkv)
+            if i == 0:      # the embedding rows are final: plain RMSNorm prologue
+                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
+                                    **rope)
+                ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            else:
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=tiles, eps=1e-6, **rope)
+                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
+            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv,
+                                fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
+            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=so)
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+            ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
+            nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
+            fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+            ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=sd)
+        return xq, ss_d, tiles
 
     def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
         """Decode layers for B > FUSE_MAX_B: the RMSNorm and the split-KV merge run once as their own
