@@ -94,7 +94,7 @@ def time_dominant_kernel(eng, reps=50):
     return avg_s, nbytes
 
 
-def cpu_baseline(cfg, ids, px, budget_tokens=3):
+def cpu_baseline(cfg, ids, px, budget_tokens=24):
     """The oracle (numpy fp32 port of the reference path) on the host: one request of the same workload,
     bounded to `budget_tokens` generated tokens (prefill + decode steps, vision re-run per call as the
     reference's modeling_paligemma.py:281 does).  Weights: the same synthetic tensors, copied from HBM."""

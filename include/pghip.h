@@ -136,6 +136,14 @@ int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature
                    const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
                    int* kv_len, float* probs_out, hipStream_t stream);
 
+/* Reference image pre-processing (processing_paligemma.py:13-73) on the device: PIL BICUBIC resize of an RGB
+ * uint8 image [H][W][3] to S x S (Pillow Resample.c fixed-point passes; tables hb/hk (horizontal, rows
+ * [y0, y0+rows) of the source) and vb/vk (vertical) from pghip/image.py; null = no pass on that axis),
+ * then out[c][y][x] = lut[u8] (rescale 1/255 + normalise).  tmp: uint8 [rows][S][3]. */
+int pg_image_preprocess(const uint8_t* src, int H, int W, int S, const int* hb, const int* hk, int hks,
+                        const int* vb, const int* vk, int vks, int y0, int rows, const float* lut, uint8_t* tmp,
+                        float* out, hipStream_t stream);
+
 /* name-seeded synthetic weights, bit-identical to oracle/synth.py (out_kind 0 bf16, 1 f32). */
 int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, int out_kind,
                   hipStream_t stream);

@@ -492,3 +492,75 @@ extern "C" int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, f
 }
 
 extern "C" int pg_abi_version(void) { return 1; }
+
+// ---------------------------------------------------------------- image pre-processing (processing_paligemma.py:13-73)
+// PIL BICUBIC resize of an RGB uint8 image (Pillow Resample.c, 22-bit fixed point, coefficient tables from
+// pghip/image.py) + the reference's rescale/normalise as a float32 lookup table, output CHW float32.
+__device__ __forceinline__ uint8_t clip8_22(int acc) {
+  const int v = acc >> 22;
+  return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+// pass 1: tmp[r][xx][c] = clip8(2^21 + sum_x src[y0 + r][xmin + x][c] * hk[xx][x])
+__global__ __launch_bounds__(256) void resize_h_kernel(const uint8_t* __restrict__ src, int W, int y0, int rows,
+                                                       int S, const int* __restrict__ hb, const int* __restrict__ hk,
+                                                       int hks, uint8_t* __restrict__ tmp) {
+  const long total = (long)rows * S * 3;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % 3), xx = (int)((i / 3) % S);
+    const long r = i / (3L * S);
+    const int xmin = hb[2 * xx], n = hb[2 * xx + 1];
+    const int* k = hk + (long)xx * hks;
+    const uint8_t* p = src + ((long)(y0 + r) * W + xmin) * 3 + c;
+    int acc = 1 << 21;
+    for (int x = 0; x < n; ++x) acc += (int)p[3 * x] * k[x];
+    tmp[i] = clip8_22(acc);
+  }
+}
+
+// pass 2: out[c][yy][xx] = lut[clip8(2^21 + sum_y in[ymin - yshift + y][xx][c] * vk[yy][y])]  (vb == null: no
+// vertical resize, out = lut[in[yy][xx][c]])
+__global__ __launch_bounds__(256) void resize_v_kernel(const uint8_t* __restrict__ in, int Win, int yshift, int S,
+                                                       const int* __restrict__ vb, const int* __restrict__ vk,
+                                                       int vks, const float* __restrict__ lut,
+                                                       float* __restrict__ out) {
+  const long total = 3L * S * S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int xx = (int)(i % S), yy = (int)((i / S) % S), c = (int)(i / ((long)S * S));
+    int v;
+    if (vb) {
+      const int ymin = vb[2 * yy] - yshift, n = vb[2 * yy + 1];
+      const int* k = vk + (long)yy * vks;
+      const uint8_t* p = in + ((long)ymin * Win + xx) * 3 + c;
+      int acc = 1 << 21;
+      for (int y = 0; y < n; ++y) acc += (int)p[(long)y * Win * 3] * k[y];
+      v = clip8_22(acc);
+    } else {
+      v = in[((long)yy * Win + xx) * 3 + c];
+    }
+    out[i] = lut[v];
+  }
+}
+
+extern "C" int pg_image_preprocess(const uint8_t* src, int H, int W, int S, const int* hb, const int* hk, int hks,
+                                   const int* vb, const int* vk, int vks, int y0, int rows, const float* lut,
+                                   uint8_t* tmp, float* out, hipStream_t stream) {
+  PG_REQUIRE(H > 0 && W > 0 && S > 0 && lut && out && src);
+  PG_REQUIRE(hb ? (hk && hks > 0 && tmp && rows > 0 && y0 >= 0 && y0 + rows <= H) : W == S);
+  PG_REQUIRE(vb ? (vk && vks > 0) : (hb ? rows == S : H == S));
+  const uint8_t* in = src;
+  int win = W, yshift = 0;
+  if (hb) {
+    const long n = (long)rows * S * 3;
+    hipLaunchKernelGGL(resize_h_kernel, dim3((int)min((n + 255) / 256, 4096L)), dim3(256), 0, stream, src, W, y0,
+                       rows, S, hb, hk, hks, tmp);
+    in = tmp;
+    win = S;
+    yshift = y0;
+  }
+  const long n = 3L * S * S;
+  hipLaunchKernelGGL(resize_v_kernel, dim3((int)min((n + 255) / 256, 4096L)), dim3(256), 0, stream, in, win, yshift,
+                     S, vb, vk, vks, lut, out);
+  PG_LAUNCH_CHECK();
+  return 0;
+}

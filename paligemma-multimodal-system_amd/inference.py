@@ -73,7 +73,8 @@ def main(model_path: str = None, prompt: str = None, image_file_path: str = None
     model, tokenizer = load_hf_model(model_path, device)
     model = model.to(device).eval()
     processor = PaliGemmaProcessor(tokenizer, model.config.vision_config.num_image_tokens or
-                                   model.config.text_config.num_image_tokens, model.config.vision_config.image_size)
+                                   model.config.text_config.num_image_tokens, model.config.vision_config.image_size,
+                                   device=device)        # resize + normalise on the device (bit-exact with PIL)
     print("Running inference")
     with torch.no_grad():
         test_inference(model, processor, device, prompt, image_file_path, max_tokens_to_generate, temperature,

@@ -44,6 +44,7 @@ SIGNATURES = {
     "pg_argmax_pairs": [vp, i64, i32, i32, i32, vp, vp, vp],
     "pg_argmax_merge": [vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp],
+    "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
 }
 

@@ -167,6 +167,13 @@ def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, ste
               _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
 
 
+def image_preprocess(src, H, W, S, hb, hk, hks, vb, vk, vks, y0, rows, lut, tmp, out):
+    _chk(src, torch.uint8, "image")
+    _chk(out, torch.float32, "pixel_values")
+    _lib.call("pg_image_preprocess", _p(src), H, W, S, _p(hb), _p(hk), hks, _p(vb), _p(vk), vks, y0, rows, _p(lut),
+              _p(tmp), _p(out), _s())
+
+
 def synth_fill(out: torch.Tensor, seedmix: int, a: float, mean: float):
     kind = 0 if out.dtype == torch.bfloat16 else 1
     if kind == 1:

@@ -52,7 +52,10 @@ class PaliGemmaProcessor:
 
     IMAGE_TOKEN = "<image>"
 
-    def __init__(self, tokenizer, num_image_tokens: int, image_size: int):
+    def __init__(self, tokenizer, num_image_tokens: int, image_size: int, device=None):
+        """device: when a HIP device is given, RGB images are resized/normalised there (pghip.image,
+        bit-exact with the host path below); None keeps the reference's host (PIL + numpy) path."""
+        self.device = device
         self.tokenizer = tokenizer
         self.image_seq_len = num_image_tokens
         self.image_size = image_size
@@ -67,8 +70,12 @@ class PaliGemmaProcessor:
         assert len(images) == 1 and len(text) == 1, \
             "Working with only 1 image and prompt, to test, got more than one"
         from PIL import Image
-        pixel_values = torch.tensor(np.stack(process_images(images, self.image_size, scale_factor=1 / 255.0,
-                                                            resampling=Image.Resampling.BICUBIC), axis=0))
+        if self.device is not None and all(getattr(im, "mode", None) == "RGB" for im in images):
+            from pghip import image as gpu_image
+            pixel_values = gpu_image.preprocess(images, self.image_size, self.device)
+        else:
+            pixel_values = torch.tensor(np.stack(process_images(images, self.image_size, scale_factor=1 / 255.0,
+                                                                resampling=Image.Resampling.BICUBIC), axis=0))
         s = create_gemma_string(prefix_prompt=text, image_seq_len=self.image_seq_len, image_token=self.IMAGE_TOKEN,
                                 bos_token=self.tokenizer.bos_token)
         toks = self.tokenizer(s, return_tensors="pt", truncation=truncation, padding=padding)

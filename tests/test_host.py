@@ -111,3 +111,17 @@ def test_kvcache_reference_api_on_static_store():
     assert torch.allclose(K2[:, :, :5].float(), k.to(torch.bfloat16).float())
     assert torch.allclose(V2[:, :, 5].float(), v[:, :, 0].to(torch.bfloat16).float())
     assert len(kv.k_cache) == 2 and kv.v_cache[1].shape == (2, 1, 5, 32)
+
+
+@pytest.mark.parametrize("H,W,S", [(480, 640, 224), (37, 51, 224), (224, 500, 224), (1000, 224, 448), (224, 224, 224)])
+def test_pil_bicubic_restatement_is_bit_exact(H, W, S):
+    """oracle/pil_resample.py + pghip.image.resample_coeffs == PIL Image.resize(BICUBIC) (Pillow 12.2.0), and the
+    normalise table == the reference's rescale/normalise (processing_paligemma.py:22-35)."""
+    from PIL import Image
+    from oracle.pil_resample import resize_u8
+    from pghip.image import normalise_lut, resample_coeffs
+    img = np.random.default_rng(H * W + S).integers(0, 256, (H, W, 3), dtype=np.uint8)
+    ref = np.array(Image.fromarray(img).resize((S, S), resample=Image.Resampling.BICUBIC))
+    assert np.array_equal(resize_u8(img, S, resample_coeffs), ref)
+    x = (np.arange(256, dtype=np.uint8) * (1 / 255.0)).astype(np.float32)
+    assert np.array_equal(normalise_lut(), (x - np.float32(0.5)) / np.float32(0.5))

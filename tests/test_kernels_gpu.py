@@ -367,3 +367,17 @@ def test_gemm_fused_qkv_rope_epilogue(M, L):
     assert err(q, qkv[:, :nh * hd]) < 1e-2
     assert err(kc, kc_r) < 1e-2
     assert err(vt, vt_r) < 1e-2
+
+
+@pytest.mark.parametrize("H,W,S", [(480, 640, 224), (37, 51, 224), (224, 500, 224), (1000, 224, 448),
+                                   (224, 224, 224), (300, 448, 448)])
+def test_image_preprocess_bit_exact_with_reference_host_path(H, W, S):
+    """pg_image_preprocess == the reference's process_images (PIL BICUBIC + rescale + normalise + CHW)."""
+    from PIL import Image
+    from processing_paligemma import process_images
+    from pghip import image
+    img = Image.fromarray(np.random.default_rng(H + W).integers(0, 256, (H, W, 3), dtype=np.uint8))
+    ref = process_images([img], S, scale_factor=1 / 255.0, resampling=Image.Resampling.BICUBIC)[0]
+    out = image.preprocess([img], S)
+    assert out.shape == (1, 3, S, S) and out.dtype == torch.float32
+    assert np.array_equal(out[0].cpu().numpy(), ref)
