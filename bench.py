@@ -94,6 +94,18 @@ def time_dominant_kernel(eng, reps=50):
     return avg_s, nbytes
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 --pmc passes
+    (scripts/gpu_pmc.sh -> profiles/*pmc_gateup.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gateup.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f)
+    return rec.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cfg, ids, px, budget_tokens=24):
     """The oracle (numpy fp32 port of the reference path) on the host: one request of the same workload,
     bounded to `budget_tokens` generated tokens (prefill + decode steps, vision re-run per call as the
@@ -267,6 +279,7 @@ def main():
 
     kern_s, kern_bytes = time_dominant_kernel(eng)
     achieved = kern_bytes / kern_s / 1e9
+    traffic, traffic_src = pmc_traffic()
     kern_desc = f"gemv_kernel<GELU_MUL,2> (decode gate/up, 2x{eng.w.inter}x{eng.w.hidden} bf16)"
 
     cpu = None
@@ -301,7 +314,8 @@ def main():
             "decode_hbm_gbs": round(decode_hbm, 1),
             "decode_hbm_frac": round(decode_hbm / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": kern_desc,
                          "kernel_avg_us": round(kern_s * 1e6, 2), "bytes_per_launch": kern_bytes},
             "cpu_baseline": cpu,

@@ -72,6 +72,8 @@ typedef struct PgFusedArgs {
   const float* ss_in;       /* pro_mode 3: producer's per-tile sums of squares [M][ss_ld], ss_n tiles          */
   int ss_ld, ss_n;
   void* fin_x;              /* PG_EPI_F32_FIN (optional): bf16 [M][N] x' = resid*(1+norm_w) for a pro_mode 4 consumer */
+  int akeys;                /* pro_mode 2: keys per attention split; with slot_dev (kv length before this token)
+                               only the non-empty splits are merged                                            */
 } PgFusedArgs;
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,

@@ -68,6 +68,8 @@ struct PgFusedArgs {
   int ss_ld, ss_n;
   bf16_t* fin_x;             // PG_EPI_F32_FIN (optional): x' = bf16(resid * (1 + norm_w)) [M][N] for a pro_mode 4
                              // consumer (x' read like A, rstd from ss_in applied to its outputs)
+  int akeys;                 // pro_mode 2: keys per attention split; with slot_dev (= kv length before this
+                             // token) only the ceil((*slot_dev + 1) / akeys) non-empty splits are merged
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -468,6 +470,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
   } else if constexpr (PRO == 2 && PG_MERGE_V2) {
     // one pass per (row, head, 4 dims): online merge over the splits, no LDS staging / barriers
     const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
+    const int Seff = (f.slot_dev && f.akeys > 0) ? min(S, (*f.slot_dev + f.akeys) / f.akeys) : S;
     const int h0 = k0 / D, nh = Kr / D, D4 = D >> 2;
     const int items = M * nh * D4;
     for (int idx = t; idx < items; idx += 256) {
@@ -477,7 +480,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
       float mx = -INFINITY, den = 0.f;
       f32x4 num = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
-      for (int sp = 0; sp < S; ++sp) {
+      for (int sp = 0; sp < Seff; ++sp) {
         const long bs = base0 + (long)sp * 16;
         const float ms = f.part_ml[bs * 2], ls = f.part_ml[bs * 2 + 1];
         const f32x4 o4 = *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);

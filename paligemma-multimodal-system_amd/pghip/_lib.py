@@ -24,7 +24,8 @@ class PgFusedArgs(C.Structure):
                 ("sin_t", C.c_void_p), ("pos", C.c_void_p), ("rows_per_batch", C.c_int), ("slot_dev", C.c_void_p),
                 ("slot_base", C.c_int), ("kc", C.c_void_p), ("vtc", C.c_void_p), ("smax", C.c_int),
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
-                ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p)]
+                ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
+                ("akeys", C.c_int)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)

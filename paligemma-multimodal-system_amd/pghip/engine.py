@@ -307,7 +307,8 @@ class PaliGemmaEngine:
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
-                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv)
+                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
+                                akeys=SK)
             ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32, M=B, ksplit=so)
             self._allreduce(part[:so])
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=so,
@@ -377,7 +378,7 @@ class PaliGemmaEngine:
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
-                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv,
+                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK,
                                 fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
             ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=so)
             fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
@@ -447,9 +448,17 @@ class PaliGemmaEngine:
 
     def generate(self, input_ids, pixel_values, attention_mask, max_new_tokens: int, do_sample=False,
                  temperature=0.8, top_p=0.9, uniforms=None, stop_token: Optional[int] = 1, use_graph=True,
-                 check_every: int = 1):
-        """test_inference's loop (inference.py:45-82): returns generated ids [B][n] (stops at EOS for B=1)."""
+                 check_every: Optional[int] = None, pad_token: int = 0, return_list: bool = False):
+        """test_inference's loop (inference.py:45-82) for B >= 1 rows.
+
+        B = 1: ids [1][n], stopping after EOS like the reference.  B > 1 (the reference asserts B = 1,
+        SURVEY §8(f2)): every row decodes in the same static-shape graph until ALL rows have produced
+        `stop_token` (checked every `check_every` steps, default 8, one host sync each) or max_new_tokens;
+        a row's tokens after its EOS are replaced by `pad_token` in the [B][n] result, or dropped when
+        return_list=True (a list of per-row id lists, each ending at its EOS)."""
         B = input_ids.shape[0]
+        if check_every is None:
+            check_every = 1 if B == 1 else 8
         cache, feats, logits, nxt = self.prefill_request(input_ids, pixel_values, attention_mask, max_new_tokens)
         st = self.decode_state(B, cache, nxt, max_new_tokens)
         sampler = dict(do_sample=do_sample, temperature=temperature, top_p=top_p)
@@ -463,18 +472,28 @@ class PaliGemmaEngine:
         step_fn = self._graph_step(st, cache, feats, sampler) if use_graph else \
             (lambda: self.decode_step(st, cache, feats, sampler))
         while n < max_new_tokens:
-            if stop_token is not None and B == 1 and (n % check_every == 0):
-                if int(st["ids"][0]) == stop_token:                       # inference.py:73-74
+            if stop_token is not None and n % check_every == 0:
+                if B == 1:
+                    if int(st["ids"][0]) == stop_token:                   # inference.py:73-74
+                        break
+                elif bool((st["hist"][:n] == stop_token).any(0).all()):   # every row has finished
                     break
             step_fn()
             n += 1
         hist = st["hist"][:n].t().contiguous().cpu()
-        if stop_token is not None and B == 1:
-            row = hist[0].tolist()
-            if stop_token in row:
-                row = row[: row.index(stop_token) + 1]
-            return torch.tensor([row], dtype=torch.int64)
-        return hist
+        if stop_token is None:
+            return [r.tolist() for r in hist] if return_list else hist
+        rows = []
+        for r in hist.tolist():
+            rows.append(r[: r.index(stop_token) + 1] if stop_token in r else r)
+        if return_list:
+            return rows
+        if B == 1:
+            return torch.tensor(rows, dtype=torch.int64)
+        out = torch.full((B, max(len(r) for r in rows)), pad_token, dtype=torch.int64)
+        for b, r in enumerate(rows):
+            out[b, : len(r)] = torch.tensor(r, dtype=torch.int64)
+        return out
 
     def _graph_step(self, st, cache, feats, sampler):
         """Capture one decode step into a hipGraph (warm-up run first, on a side stream)."""

@@ -181,3 +181,21 @@ def test_pt224_full_size_teacher_forced_decode(golden):
             assert int(np.argmax(lg)) == int(g["greedy_ids"][t]), (t, e, float(g["margin"][t]))
             checked += 1
     assert checked >= 4, checked
+
+
+def test_batched_generation_per_row_eos(tiny, golden):
+    """B = 2 rows of the same request (+ one different image): each row equals its own B = 1 run, cut at
+    its own EOS (tokens after a row's EOS come back as pad)."""
+    eng, _ = tiny
+    g = golden("tiny")
+    ids1 = torch.from_numpy(g["b1_input_ids"]).cuda()
+    px1 = torch.from_numpy(g["b1_pixel_values"]).cuda()
+    px2 = torch.from_numpy(g["b2_pixel_values"][1:2]).cuda()
+    single = [eng.generate(ids1, p, torch.ones_like(ids1), 12)[0].tolist() for p in (px1, px2)]
+    ids = ids1.repeat(2, 1)
+    rows = eng.generate(ids, torch.cat([px1, px2]), torch.ones_like(ids), 12, return_list=True)
+    assert rows == single
+    out = eng.generate(ids, torch.cat([px1, px2]), torch.ones_like(ids), 12, pad_token=0)
+    for b in range(2):
+        assert out[b, : len(single[b])].tolist() == single[b]
+        assert (out[b, len(single[b]):] == 0).all()
