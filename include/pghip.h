@@ -138,6 +138,32 @@ int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature
                    const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
                    int* kv_len, float* probs_out, hipStream_t stream);
 
+/* Persistent decode MLP for batch <= 2 (GemmaMLP.forward, modeling_gemma.py:210-218, + the residual add of
+ * DecoderLayer :412-416 + the next RMSNorm's statistics) in one launch: gate/up GEMV with gelu*mul, a grid
+ * barrier, then the down GEMV in Z split-K slices finalised in-kernel (resid += slabs, x_out = bf16(resid *
+ * (1 + norm_w_next)), per-16-column-tile sums of squares in ss_out).  x is the previous finalisation's x',
+ * rstd from ss_in.  One workgroup per CU; bar is a monotonic 64-bit ticket (zero once, never reset); a
+ * barrier spin that gives up sets *err. */
+typedef struct PgMlpArgs {
+  const void* x;            /* bf16 [M][H] */
+  const float* ss_in;       /* [M][ss_ld], ss_n tiles */
+  int ss_ld, ss_n;
+  float eps;
+  const void* gu_w;         /* bf16 [2I][H], gate/up interleaved in 16-row blocks */
+  void* h;                  /* bf16 [M][I] scratch */
+  const void* down_w;       /* bf16 [H][I] */
+  float* part;              /* [Z][M][H] */
+  int* fin_cnt;             /* [H/16], zero */
+  float* resid;             /* [M][H] */
+  float* ss_out;            /* [M][ss_ld] */
+  void* x_out;              /* bf16 [M][H] */
+  const float* norm_w_next;
+  unsigned long long* bar;
+  int* err;
+  int M, H, I, Z;
+} PgMlpArgs;
+int pg_decode_mlp(const PgMlpArgs* args, hipStream_t stream);
+
 /* Reference image pre-processing (processing_paligemma.py:13-73) on the device: PIL BICUBIC resize of an RGB
  * uint8 image [H][W][3] to S x S (Pillow Resample.c fixed-point passes; tables hb/hk (horizontal, rows
  * [y0, y0+rows) of the source) and vb/vk (vertical) from pghip/image.py; null = no pass on that axis),

@@ -369,6 +369,9 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #ifndef PG_GEMV_NT
 #define PG_GEMV_NT 0
 #endif
+#ifndef PG_GEMV_CONTIG
+#define PG_GEMV_CONTIG 0
+#endif
 #ifndef PG_TIMING_NOPRO
 #define PG_TIMING_NOPRO 0
 #endif
@@ -591,30 +594,35 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   }
   const bf16_t* xlds = xs + (xvalid ? r : 0) * (Kr + XPAD);
 
+  // element offset of a lane's 16-B piece s inside a CH-element chunk: PG_GEMV_CONTIG lays piece s of the 4
+  // lane groups side by side (one load instruction = 64 contiguous bytes per row); otherwise a lane owns 16U
+  // contiguous elements.  x uses the same map, so the k order inside the MFMA is consistent either way.
+  constexpr int S_STRIDE = PG_GEMV_CONTIG ? 32 : 8;
+  const int LANE_OFF = PG_GEMV_CONTIG ? g * 8 : g * 8 * U;
   u32x4 wb[DEPTH][NT][U];
   u32x4 xb[DEPTH][U];
   auto loadw = [&](int j, u32x4 (&wv)[NT][U]) {
-    const int off = (c0 + wave + j * 4) * CH + g * 8 * U;
+    const int off = (c0 + wave + j * 4) * CH + LANE_OFF;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int s = 0; s < U; ++s) {
 #if PG_GEMV_NT
-        wv[t][s] = __builtin_nontemporal_load((const u32x4*)(wrow[t] + off + 8 * s));
+        wv[t][s] = __builtin_nontemporal_load((const u32x4*)(wrow[t] + off + S_STRIDE * s));
 #else
-        wv[t][s] = *(const u32x4*)(wrow[t] + off + 8 * s);
+        wv[t][s] = *(const u32x4*)(wrow[t] + off + S_STRIDE * s);
 #endif
       }
   };
   auto loadx = [&](int j, u32x4 (&xv)[U]) {
-    const int koff = (wave + j * 4) * CH + g * 8 * U;     // offset inside this split
+    const int koff = (wave + j * 4) * CH + LANE_OFF;      // offset inside this split
     if constexpr (PRO == 0 || PRO == 4) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
-        xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
+        xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
     } else {
 #pragma unroll
-      for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + 8 * s) : u32x4{0u, 0u, 0u, 0u};
+      for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
     }
   };
   constexpr bool STAGED = PRO != 0 && PRO != 4;   // x built in LDS by a prologue

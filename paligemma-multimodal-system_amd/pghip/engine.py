@@ -67,6 +67,10 @@ class PaliGemmaEngine:
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
+    PERSIST_MLP = False     # with USE_FIN: gate/up + down in one persistent launch (pg_decode_mlp); measured
+                            # slower (57-64 us vs 48 us for the two launches): its write-through h is re-read
+                            # past L2 by every wave -- kept, tested, off until h is staged through LDS
+    MLP_SPLIT_DOWN = 8      # K slices of the persistent down projection (one wave per tile x slice)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -360,6 +364,12 @@ class PaliGemmaEngine:
         ss_o = self._buf("d_ss_o", (B, tiles), torch.float32)
         ss_d = self._buf("d_ss_d", (B, tiles), torch.float32)
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
+        bar = self._zeros("d_grid_bar", (1,), torch.int64)          # monotonic grid-barrier ticket
+        err = self._zeros("d_grid_err", (1,), torch.int32)
+        zm = self.MLP_SPLIT_DOWN                                      # K slices: I/Z a multiple of 32
+        while zm > 1 and (w.inter % zm or (w.inter // zm) % 32):
+            zm -= 1
+        mlp_part = self._buf("d_mlp_part", (zm, B, H), torch.float32)
         SK = self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
         for i, Lw in enumerate(w.tl):
@@ -381,11 +391,17 @@ class PaliGemmaEngine:
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK,
                                 fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
             ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=so)
-            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
-            ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
-            ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=sd)
+            if self.PERSIST_MLP:
+                # gate/up -> grid barrier -> down + finalisation in one launch (csrc/decode_mlp.hip)
+                ops.decode_mlp(x=xq, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6, gu_w=Lw["gu_w"], h=h,
+                               down_w=Lw["down_w"], part=mlp_part, fin_cnt=cnt, resid=res, ss_out=ss_d, x_out=xq,
+                               norm_w_next=nxt_w, bar=bar, err=err, M=B, H=H, I=w.inter, Z=zm)
+            else:
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+                ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
+                fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+                ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=sd)
         return xq, ss_d, tiles
 
     def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):

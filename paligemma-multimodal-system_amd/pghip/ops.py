@@ -167,6 +167,14 @@ def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, ste
               _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
 
 
+def decode_mlp(**kw):
+    """pg_decode_mlp: persistent gate/up -> grid barrier -> down + finalisation (batch <= 2)."""
+    a = _lib.PgMlpArgs()
+    for k, v in kw.items():
+        setattr(a, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
+    _lib.call("pg_decode_mlp", _lib.C.byref(a), _s())
+
+
 def image_preprocess(src, H, W, S, hb, hk, hks, vb, vk, vks, y0, rows, lut, tmp, out):
     _chk(src, torch.uint8, "image")
     _chk(out, torch.float32, "pixel_values")
