@@ -80,13 +80,13 @@ def time_dominant_kernel(eng, reps=50):
     x = torch.randn(1, w.hidden, device="cuda").to(torch.bfloat16)
     h = torch.empty(1, w.inter, dtype=torch.bfloat16, device="cuda")
     for _ in range(5):
-        ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+        ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
     # rotate over the 18 layers' weights so every launch streams from HBM (no L2/MALL reuse)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     ev0.record()
     for i in range(reps):
-        ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+        ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
     ev1.record()
     torch.cuda.synchronize()
     avg_s = ev0.elapsed_time(ev1) / 1e3 / reps

@@ -76,6 +76,13 @@ typedef struct PgFusedArgs {
                                only the non-empty splits are merged                                            */
 } PgFusedArgs;
 
+/* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
+ * the HBM layout of the Gemma decoder weights (pghip/weights.py frag_pack): for 16-row block t and 64-wide
+ * k chunk c, W[16t + r][64c + 16g + 8s + e] (r < 16, g < 4, s < 2, e < 8) is stored at element
+ * ((((t * K/64 + c) * 2 + s) * 64 + 16g + r) * 8 + e): each GEMV wave-instruction then reads 1 KiB
+ * contiguous, lane-linear.  Requires N % 16 == 0 and K % 64 == 0; ldw must equal K. */
+#define PG_W_FRAG 0x100
+
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
  * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0
  * (% 64 when M > 16), N % 4 == 0.  M <= 16 takes the weight-streaming GEMV path. */
@@ -138,32 +145,6 @@ int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature
                    const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
                    int* kv_len, float* probs_out, hipStream_t stream);
 
-/* Persistent decode MLP for batch <= 2 (GemmaMLP.forward, modeling_gemma.py:210-218, + the residual add of
- * DecoderLayer :412-416 + the next RMSNorm's statistics) in one launch: gate/up GEMV with gelu*mul, a grid
- * barrier, then the down GEMV in Z split-K slices finalised in-kernel (resid += slabs, x_out = bf16(resid *
- * (1 + norm_w_next)), per-16-column-tile sums of squares in ss_out).  x is the previous finalisation's x',
- * rstd from ss_in.  One workgroup per CU; bar is a monotonic 64-bit ticket (zero once, never reset); a
- * barrier spin that gives up sets *err. */
-typedef struct PgMlpArgs {
-  const void* x;            /* bf16 [M][H] */
-  const float* ss_in;       /* [M][ss_ld], ss_n tiles */
-  int ss_ld, ss_n;
-  float eps;
-  const void* gu_w;         /* bf16 [2I][H], gate/up interleaved in 16-row blocks */
-  void* h;                  /* bf16 [M][I] scratch */
-  const void* down_w;       /* bf16 [H][I] */
-  float* part;              /* [Z][M][H] */
-  int* fin_cnt;             /* [H/16], zero */
-  float* resid;             /* [M][H] */
-  float* ss_out;            /* [M][ss_ld] */
-  void* x_out;              /* bf16 [M][H] */
-  const float* norm_w_next;
-  unsigned long long* bar;
-  int* err;
-  int M, H, I, Z;
-} PgMlpArgs;
-int pg_decode_mlp(const PgMlpArgs* args, hipStream_t stream);
-
 /* Reference image pre-processing (processing_paligemma.py:13-73) on the device: PIL BICUBIC resize of an RGB
  * uint8 image [H][W][3] to S x S (Pillow Resample.c fixed-point passes; tables hb/hk (horizontal, rows
  * [y0, y0+rows) of the source) and vb/vk (vertical) from pghip/image.py; null = no pass on that axis),
@@ -175,6 +156,10 @@ int pg_image_preprocess(const uint8_t* src, int H, int W, int S, const int* hb, 
 /* name-seeded synthetic weights, bit-identical to oracle/synth.py (out_kind 0 bf16, 1 f32). */
 int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, int out_kind,
                   hipStream_t stream);
+
+/* Read [p, p + bytes) and discard it (weights pulled into the Infinity Cache ahead of the kernel that
+ * streams them; no reference counterpart: a scheduling aid of the decode graph).  policy 1 = nt loads. */
+int pg_prefetch(const void* p, long bytes, int wgs, int policy, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,8 @@ __device__ __forceinline__ f32x4 load4_guard(const float* __restrict__ p, int n0
   return v;
 }
 
+#define PG_W_FRAG 0x100   // weight layout flag OR-ed into epi (include/pghip.h)
+
 struct EpiArgs {
   const float* bias;
   void* C;
@@ -213,8 +215,14 @@ __device__ __forceinline__ void epi_gelu_mul4(const EpiArgs& e, int m, int gb, i
 #define TBN 128
 #define TBK 64
 
-// Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread over the 4 waves.
-template <int ROWS>
+// element offset of W[row][k0 + 8c .. +8) (k0 % 64 == 0, c < 8) in the fragment-packed layout (PG_W_FRAG)
+__device__ __forceinline__ size_t frag_off(int row, int k0, int c, int K) {
+  return (size_t)(row >> 4) * 16 * K + ((size_t)(k0 >> 6) * 2 + (c & 1)) * 512 + ((c >> 1) * 16 + (row & 15)) * 8;
+}
+
+// Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread over the 4 waves.  FRAG: src is fragment-packed
+// (ld = K); each piece still reads 8 runs of 128 contiguous bytes.
+template <int ROWS, bool FRAG = false>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int rows_valid,
                                            int k0, char* lds_tile, int wave, int lane) {
   constexpr int PER_WAVE = ROWS / 32;
@@ -225,7 +233,7 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int l
     const int c = (lane & 7) ^ ((r >> 1) & 7);     // logical 16-B chunk landing at physical chunk lane&7
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
-    const bf16_t* g = src + (size_t)gr * ld + k0 + c * 8;
+    const bf16_t* g = FRAG ? src + frag_off(gr, k0, c, ld) : src + (size_t)gr * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (LDS_AS void*)(lds_tile + blk * 1024), 16, 0, 0);
   }
 }
@@ -248,7 +256,7 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
   }
 }
 
-template <int EPI, int BM, int STAGES>
+template <int EPI, int BM, int STAGES, bool FRAG>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W, int ldw, int K, int kchunk,
                                                         int tiles_m, int tiles_n, EpiArgs e) {
@@ -294,7 +302,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE_BYTES;
     stage_tile<BM>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
-    stage_tile<TBN>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
+    stage_tile<TBN, FRAG>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
   };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -372,8 +380,14 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
 #endif
-#ifndef PG_TIMING_NOPRO
-#define PG_TIMING_NOPRO 0
+#ifndef PG_GEMV_D2
+#define PG_GEMV_D2 4
+#endif
+#ifndef PG_GEMV_XLDS
+#define PG_GEMV_XLDS 0
+#endif
+#ifndef PG_GEMV_FRAG_NT
+#define PG_GEMV_FRAG_NT 1
 #endif
 #ifndef PG_MERGE_V2
 #define PG_MERGE_V2 1
@@ -381,11 +395,18 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 
 template <int PRO>
 __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, int k0, int Kr, bf16_t* xs,
-                                              float* scratch) {
+                                              float* scratch, const bf16_t* __restrict__ A, int lda) {
   const PgFusedArgs& f = e.f;
   const int t = threadIdx.x;
   const int ldx = Kr + XPAD;
-  if constexpr (PRO == 1) {
+  if constexpr (PRO == 0 || PRO == 4) {
+    // x rows [M][k0, k0 + Kr) copied from A into LDS (PG_GEMV_XLDS): one L2 read per workgroup
+    const int K8 = Kr >> 3;
+    for (int idx = t; idx < M * K8; idx += 256) {
+      const int m = idx / K8, c = idx % K8;
+      *(u32x4*)(xs + m * ldx + c * 8) = *(const u32x4*)(A + (size_t)m * lda + k0 + c * 8);
+    }
+  } else if constexpr (PRO == 1) {
     // RMSNorm over the FULL row (Kr == K): pass 1 sum of squares, pass 2 normalise into LDS
     const int K4 = K >> 2;
     const bool w0 = blockIdx.x == 0 && blockIdx.y == 0 && f.resid_out != nullptr;
@@ -543,7 +564,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
   __syncthreads();
 }
 
-template <int EPI, int NT, int U, int DEPTH, int PRO>
+template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
                                                    const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
   constexpr int CH = U * 32;
@@ -564,11 +585,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   const int mine = nch > wave ? (nch - wave + 3) / 4 : 0;   // chunks wave, wave+4, ...
 
   const bf16_t* wrow[NT];
+  const bf16_t* wfrag[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     int n = (tile0 + t) * 16 + r;
     n = n < e.N ? n : e.N - 1;
     wrow[t] = W + (size_t)n * ldw;
+    wfrag[t] = W + (size_t)min(tile0 + t, (e.N >> 4) - 1) * 16 * ldw;
   }
   f32x4 acc[NT];
 #pragma unroll
@@ -602,21 +625,38 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   u32x4 wb[DEPTH][NT][U];
   u32x4 xb[DEPTH][U];
   auto loadw = [&](int j, u32x4 (&wv)[NT][U]) {
-    const int off = (c0 + wave + j * 4) * CH + LANE_OFF;
+    if constexpr (FRAG) {
+      // fragment-packed weights: tile t's chunk c is U wave-instructions of 1 KiB, lane-linear; read once,
+      // so non-temporal (measured: gate/up 28.7 -> 23.0 us, down 17.0 -> 13.8 us vs row-major plain loads)
+      const int cc = c0 + wave + j * 4;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int s = 0; s < U; ++s) {
-#if PG_GEMV_NT
-        wv[t][s] = __builtin_nontemporal_load((const u32x4*)(wrow[t] + off + S_STRIDE * s));
+        for (int s = 0; s < U; ++s) {
+          const u32x4* src = (const u32x4*)(wfrag[t] + ((size_t)cc * U + s) * 512 + lane * 8);
+#if PG_GEMV_FRAG_NT
+          wv[t][s] = __builtin_nontemporal_load(src);
 #else
-        wv[t][s] = *(const u32x4*)(wrow[t] + off + S_STRIDE * s);
+          wv[t][s] = *src;
 #endif
-      }
+        }
+    } else {
+      const int off = (c0 + wave + j * 4) * CH + LANE_OFF;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int s = 0; s < U; ++s) {
+#if PG_GEMV_NT
+          wv[t][s] = __builtin_nontemporal_load((const u32x4*)(wrow[t] + off + S_STRIDE * s));
+#else
+          wv[t][s] = *(const u32x4*)(wrow[t] + off + S_STRIDE * s);
+#endif
+        }
+    }
   };
   auto loadx = [&](int j, u32x4 (&xv)[U]) {
     const int koff = (wave + j * 4) * CH + LANE_OFF;      // offset inside this split
-    if constexpr (PRO == 0 || PRO == 4) {
+    if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
         xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
@@ -625,7 +665,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
     }
   };
-  constexpr bool STAGED = PRO != 0 && PRO != 4;   // x built in LDS by a prologue
+  constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
   if constexpr (STAGED && PG_GEMV_PREW) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
@@ -633,7 +673,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   }
   if constexpr (STAGED) {
     float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
-    gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch);
+    gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch, A, lda);
   }
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
@@ -768,7 +808,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 // Tile choice: 128-row tiles (2-stage ring, 64 KiB LDS -> 2 workgroups per CU) when that grid already
 // has >= 256 workgroups; otherwise 64-row tiles with a 4-stage ring.  Split-K (fp32 partial epilogue
 // only) is chosen by the caller.
-template <int EPI>
+template <int EPI, bool FRAG>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
   const int tiles_n = (e.N + TBN - 1) / TBN;
@@ -776,26 +816,26 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   const int t128 = ((e.M + 127) / 128) * tiles_n;
   if (t128 >= 256) {
     const int tiles_m = (e.M + 127) / 128;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st, A,
-                       lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st,
+                       A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
     return;
   }
   // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
   const int m64 = (e.M + 63) / 64;
-  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda, W,
-                     ldw, K, kchunk, m64, tiles_n, e);
+  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+                     W, ldw, K, kchunk, m64, tiles_n, e);
 }
 
 // measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
 // M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
-template <int EPI, int PRO>
+template <int EPI, int PRO, bool FRAG>
 static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
   const int ntiles = (e.N + 15) / 16;
   const int CH = 64;                                   // U = 2
   const int per_z = (K / CH + ksplit - 1) / ksplit;
   size_t lds = 0;
-  if (PRO != 0 && PRO != 4) {
+  if ((PRO != 0 && PRO != 4) || PG_GEMV_XLDS) {
     lds = (size_t)e.M * (per_z * CH + XPAD) * 2;
     lds = (lds + 15) & ~(size_t)15;
     if (PRO == 1) lds += 64 * sizeof(float);
@@ -807,37 +847,47 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   }
   if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
     dim3 grid((ntiles + 1) / 2, ksplit);
-    hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, 4, PRO>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
+    hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
+                       e);
   } else {
     dim3 grid(ntiles, ksplit);
-    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, 8, PRO>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
+    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, 8, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
   }
 }
 
-template <int EPI>
+template <int EPI, bool FRAG>
 static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
-#if PG_TIMING_NOPRO   // timing experiment only (wrong numerics): the fused prologues replaced by a plain x read
-  if (e.f.pro_mode != 0) {
-    const bf16_t* xa = (const bf16_t*)(e.f.pro_mode == 1 ? (const void*)e.f.resid_in : (const void*)e.f.part_o);
-    launch_gemv_pro<EPI, 0>(xa, K, W, ldw, K, ksplit, e, st);
-    return;
-  }
-#endif
   switch (e.f.pro_mode) {
-    case 1: launch_gemv_pro<EPI, 1>(A, lda, W, ldw, K, ksplit, e, st); break;
-    case 2: launch_gemv_pro<EPI, 2>(A, lda, W, ldw, K, ksplit, e, st); break;
-    case 3: launch_gemv_pro<EPI, 3>(A, lda, W, ldw, K, ksplit, e, st); break;
-    case 4: launch_gemv_pro<EPI, 4>(A, lda, W, ldw, K, ksplit, e, st); break;
-    default: launch_gemv_pro<EPI, 0>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 1: launch_gemv_pro<EPI, 1, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 2: launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 3: launch_gemv_pro<EPI, 3, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 4: launch_gemv_pro<EPI, 4, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    default: launch_gemv_pro<EPI, 0, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
   }
+}
+
+// M <= 16 -> weight-streaming GEMV, else the tile GEMM; FRAG (PG_W_FRAG) only for the Gemma epilogues
+template <int EPI, bool FRAG>
+static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
+                       hipStream_t st) {
+  if (e.M <= 16)
+    launch_gemv<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+  else if constexpr (EPI != PG_EPI_F32_FIN)
+    launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
 }
 
 static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
-                     int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
+                     int M, int N, int K, int epi_flags, int ksplit, const float* aux, int aux_rows, void* aux_out,
                      int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
+  const bool frag = (epi_flags & PG_W_FRAG) != 0;
+  const int epi = epi_flags & 0xFF;
+  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG)) == 0);
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
+  if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
+                       (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||
+                        epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN));
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
@@ -859,34 +909,30 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
   if (epi == PG_EPI_BF16_VT) PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
+  if (M <= 16) PG_REQUIRE(K % 64 == 0);
+  else PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0 && epi != PG_EPI_F32_FIN);
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
-  if (M <= 16) {
-    PG_REQUIRE(K % 64 == 0);
-    switch (epi) {
-      case PG_EPI_BF16: launch_gemv<PG_EPI_BF16>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU: launch_gemv<PG_EPI_BF16_GELU>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU_MUL: launch_gemv<PG_EPI_BF16_GELU_MUL>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32: launch_gemv<PG_EPI_F32>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32_POS: launch_gemv<PG_EPI_F32_POS>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_VT: launch_gemv<PG_EPI_BF16_VT>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_QKV_ROPE: launch_gemv<PG_EPI_QKV_ROPE>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32_FIN: launch_gemv<PG_EPI_F32_FIN>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      default: return (int)hipErrorInvalidValue;
-    }
-  } else {
-    PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0);
-    switch (epi) {
-      case PG_EPI_BF16: launch_tile<PG_EPI_BF16>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU: launch_tile<PG_EPI_BF16_GELU>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_GELU_MUL: launch_tile<PG_EPI_BF16_GELU_MUL>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32: launch_tile<PG_EPI_F32>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_F32_POS: launch_tile<PG_EPI_F32_POS>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_BF16_VT: launch_tile<PG_EPI_BF16_VT>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      case PG_EPI_QKV_ROPE: launch_tile<PG_EPI_QKV_ROPE>(a, lda, w, ldw, K, ksplit, e, stream); break;
-      default: return (int)hipErrorInvalidValue;
-    }
+#define PG_CASE(E)                                                                             \
+  case E:                                                                                      \
+    if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream);                       \
+    else launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream);                           \
+    break;
+#define PG_CASE_ROWMAJOR(E)                                                                    \
+  case E: launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream); break;
+  switch (epi) {
+    PG_CASE(PG_EPI_BF16)
+    PG_CASE(PG_EPI_BF16_GELU_MUL)
+    PG_CASE(PG_EPI_F32)
+    PG_CASE(PG_EPI_QKV_ROPE)
+    PG_CASE(PG_EPI_F32_FIN)
+    PG_CASE_ROWMAJOR(PG_EPI_BF16_GELU)
+    PG_CASE_ROWMAJOR(PG_EPI_F32_POS)
+    PG_CASE_ROWMAJOR(PG_EPI_BF16_VT)
+    default: return (int)hipErrorInvalidValue;
   }
+#undef PG_CASE
+#undef PG_CASE_ROWMAJOR
   PG_LAUNCH_CHECK();
   return 0;
 }

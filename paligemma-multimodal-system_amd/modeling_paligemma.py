@@ -166,7 +166,7 @@ class PaliGemmaForConditionalGeneration(nn.Module):
                         + torch.arange(L - k, L, device=dev, dtype=torch.int32)[None]).reshape(-1).contiguous()
             logits, _ = eng.gemma_prefill(resid, pos, store, B, L, logits_rows=rows)
             cache.adopt(store, L, w.kv_heads, w.head_dim)
-            logits = logits.view(B, -1, w.vocab)
+            logits = logits.reshape(B, -1, w.vocab)
         else:
             assert L == 1, "Generation Phase more than one token CAN'T be input"
             feats = cache.image_features
@@ -177,7 +177,7 @@ class PaliGemmaForConditionalGeneration(nn.Module):
             st = {"ids": input_ids.reshape(B).contiguous(),
                   "pos": attention_mask.sum(-1).to(torch.int32).reshape(B).contiguous(),
                   "kv_len": torch.full((1,), n, dtype=torch.int32, device=dev)}
-            logits = eng.decode_step(st, store, feats, sampler=None).clone().view(B, 1, w.vocab)
+            logits = eng.decode_step(st, store, feats, sampler=None).reshape(B, 1, w.vocab).clone()
             cache._len = [n + 1] * len(cache._len)
         return {"logits": logits, "kv_cache": cache}
 

@@ -28,15 +28,6 @@ class PgFusedArgs(C.Structure):
                 ("akeys", C.c_int)]
 
 
-class PgMlpArgs(C.Structure):
-    """Mirror of PgMlpArgs (include/pghip.h)."""
-    _fields_ = [("x", C.c_void_p), ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int),
-                ("eps", C.c_float), ("gu_w", C.c_void_p), ("h", C.c_void_p), ("down_w", C.c_void_p),
-                ("part", C.c_void_p), ("fin_cnt", C.c_void_p), ("resid", C.c_void_p), ("ss_out", C.c_void_p),
-                ("x_out", C.c_void_p), ("norm_w_next", C.c_void_p), ("bar", C.c_void_p), ("err", C.c_void_p),
-                ("M", C.c_int), ("H", C.c_int), ("I", C.c_int), ("Z", C.c_int)]
-
-
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
 SIGNATURES = {
     "pg_abi_version": [],
@@ -54,9 +45,9 @@ SIGNATURES = {
     "pg_argmax_pairs": [vp, i64, i32, i32, i32, vp, vp, vp],
     "pg_argmax_merge": [vp, i32, i32, vp, vp, vp, vp, vp, vp],
     "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp],
-    "pg_decode_mlp": [C.POINTER(PgMlpArgs), vp],
     "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
+    "pg_prefetch": [vp, i64, i32, i32, vp],
 }
 
 _lib = None

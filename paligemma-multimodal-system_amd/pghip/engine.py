@@ -67,10 +67,6 @@ class PaliGemmaEngine:
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
-    PERSIST_MLP = False     # with USE_FIN: gate/up + down in one persistent launch (pg_decode_mlp); measured
-                            # slower (57-64 us vs 48 us for the two launches): its write-through h is re-read
-                            # past L2 by every wave -- kept, tested, off until h is staged through LDS
-    MLP_SPLIT_DOWN = 8      # K slices of the persistent down projection (one wave per tile x slice)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -200,17 +196,17 @@ class PaliGemmaEngine:
             # q|k|v projection + RoPE + KV-cache append in one GEMM (modeling_gemma.py:274-302)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=0,
                                 kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
-            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=T)
+            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=T)
             ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
                           mask_rs=(mask.stride(-2) if mask is not None else 0))
-            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=s_o)
+            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=s_o)
             self._allreduce(part[:s_o])
             ops.norm_residual(x_resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=s_o, out=xn)
-            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=s_d)
+            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=s_d)
             self._allreduce(part[:s_d])
             ns = s_d
             if taps is not None:
@@ -236,13 +232,13 @@ class PaliGemmaEngine:
         alloc = (lambda shape: torch.empty(*shape, dtype=torch.float32, device=self.device)) if fresh else \
             (lambda shape: self._buf(name, shape, torch.float32))
         if self.tp == 1:
-            logits = alloc((rows, w.vocab))
-            ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32, bias=w.lm_bias)
-            return logits
+            logits = alloc((rows, w.vocab_local_pad))      # lm_w rows padded to 16 (fragment packing)
+            ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
+            return logits[:, :w.vocab]
         vl, vlp = w.vocab_local, w.vocab_local_pad                       # 16-byte aligned slots
         g = alloc((rows, self.tp, vlp))
         g.zero_()
-        ops.gemm(xf, w.lm_w, g[:, self.comm.rank], epi=ops.EPI_F32, bias=w.lm_bias, M=rows)  # pad rows give 0
+        ops.gemm(xf, w.lm_w, g[:, self.comm.rank], epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias, M=rows)  # pad rows give 0
         self._allreduce(g)
         return g.view(rows, w.vocab) if vlp == vl else g[:, :, :vl].reshape(rows, w.vocab)
 
@@ -294,9 +290,10 @@ class PaliGemmaEngine:
             xq, ss, tiles = self._decode_layers_fin(st, cache, res_a, qb, h, part, part_o, part_ml, nsplit, dt,
                                                     cos_t, sin_t)
             # final RMSNorm folded into the lm_head GEMV: x' = resid*(1+w) from the last down_proj, rstd on the outputs
-            logits = self._buf("d_logits", (B, w.vocab), torch.float32)
+            logits = self._buf("d_logits", (B, w.vocab_local_pad), torch.float32)
             fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=tiles, ss_n=tiles, eps=1e-6)
-            ops.gemm_fused(xq, w.lm_w, logits, fa, epi=ops.EPI_F32, M=B, bias=w.lm_bias)
+            ops.gemm_fused(xq, w.lm_w, logits, fa, epi=ops.EPI_F32 | w.wflag, M=B, bias=w.lm_bias)
+            logits = logits[:, :w.vocab]
             if sampler is not None:
                 self.sample(logits, st, sampler, advance=True)
             return logits
@@ -305,7 +302,7 @@ class PaliGemmaEngine:
                                 norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
                                 rows_per_batch=1, slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i],
                                 vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
-            ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
@@ -313,19 +310,19 @@ class PaliGemmaEngine:
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                 akeys=SK)
-            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32, M=B, ksplit=so)
+            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32 | w.wflag, M=B, ksplit=so)
             self._allreduce(part[:so])
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=so,
                                 norm_w=Lw["post_w"], eps=1e-6)
-            ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=sd)
+            ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=sd)
             self._allreduce(part[:sd])
             ns = sd
         ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
         if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
             # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
             loc = self._buf("d_logits_loc", (B, w.vocab_local_pad), torch.float32)
-            ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32, bias=w.lm_bias)
+            ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
             loc = loc[:, :w.vocab_local]
             pairs = self._buf("d_pairs", (self.tp, B, 2), torch.float32)
             pairs.zero_()
@@ -364,12 +361,6 @@ class PaliGemmaEngine:
         ss_o = self._buf("d_ss_o", (B, tiles), torch.float32)
         ss_d = self._buf("d_ss_d", (B, tiles), torch.float32)
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
-        bar = self._zeros("d_grid_bar", (1,), torch.int64)          # monotonic grid-barrier ticket
-        err = self._zeros("d_grid_err", (1,), torch.int32)
-        zm = self.MLP_SPLIT_DOWN                                      # K slices: I/Z a multiple of 32
-        while zm > 1 and (w.inter % zm or (w.inter // zm) % 32):
-            zm -= 1
-        mlp_part = self._buf("d_mlp_part", (zm, B, H), torch.float32)
         SK = self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
         for i, Lw in enumerate(w.tl):
@@ -379,10 +370,10 @@ class PaliGemmaEngine:
             if i == 0:      # the embedding rows are final: plain RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                     **rope)
-                ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+                ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=tiles, eps=1e-6, **rope)
-                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
@@ -390,18 +381,12 @@ class PaliGemmaEngine:
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK,
                                 fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
-            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=so)
+            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            if self.PERSIST_MLP:
-                # gate/up -> grid barrier -> down + finalisation in one launch (csrc/decode_mlp.hip)
-                ops.decode_mlp(x=xq, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6, gu_w=Lw["gu_w"], h=h,
-                               down_w=Lw["down_w"], part=mlp_part, fin_cnt=cnt, resid=res, ss_out=ss_d, x_out=xq,
-                               norm_w_next=nxt_w, bar=bar, err=err, M=B, H=H, I=w.inter, Z=zm)
-            else:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
-                ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL, M=B)
-                fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
-                ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN, M=B, ksplit=sd)
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+            ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+            fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+            ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
         return xq, ss_d, tiles
 
     def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
@@ -419,18 +404,18 @@ class PaliGemmaEngine:
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv)
-            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE, M=B)
+            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=self.DECODE_SPLIT_KEYS, nsplit=nsplit, part_o=part_o,
                           part_ml=part_ml)
             ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
-            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32, ksplit=so)
+            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=so)
             self._allreduce(part[:so])
             ops.norm_residual(res, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=so, out=xn)
-            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32, ksplit=sd)
+            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
+            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=sd)
             self._allreduce(part[:sd])
             ns = sd
         return ns

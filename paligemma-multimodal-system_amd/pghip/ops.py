@@ -16,6 +16,7 @@ from . import _lib
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN = range(8)
 PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
 NORM_LAYER, NORM_RMS = 0, 1
+W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -33,13 +34,21 @@ def _chk(t: torch.Tensor, dtype, name: str):
         raise TypeError(f"pghip: {name} must be {dtype}, got {t.dtype}")
 
 
+def _chk_frag(W: torch.Tensor, epi: int):
+    if epi & W_FRAG and (W.shape[0] % 16 or W.shape[1] % 64 or W.stride(0) != W.shape[1]):
+        raise ValueError(f"pghip: a fragment-packed W must be [N%16][K%64] and contiguous, got {tuple(W.shape)}")
+
+
 def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_BF16,
          bias: Optional[torch.Tensor] = None, ksplit: int = 1, N: Optional[int] = None,
          aux: Optional[torch.Tensor] = None, aux_rows: int = 0, aux_out: Optional[torch.Tensor] = None,
          aux_ld: int = 0, aux_n: int = 0, M: Optional[int] = None) -> torch.Tensor:
-    """out = epilogue(A[M][K] . W[N][K]^T).  K = W.shape[1] (zero-padded), A.shape[1] >= K."""
+    """out = epilogue(A[M][K] . W[N][K]^T).  K = W.shape[1] (zero-padded), A.shape[1] >= K.
+    epi may carry W_FRAG (W fragment-packed, weights.frag_pack)."""
     _chk(A, torch.bfloat16, "A")
     _chk(W, torch.bfloat16, "W")
+    _chk_frag(W, epi)
+    flags, epi = epi, epi & 0xFF
     if A.stride(1) != 1 or W.stride(1) != 1 or out.stride(-1) != 1:
         raise ValueError("pghip.gemm: inner dims must be contiguous")
     M = A.shape[0] if M is None else M
@@ -61,7 +70,7 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
         _chk(out, torch.bfloat16, "out")
     if M > 16 and K % 64:
         raise ValueError("pghip.gemm: K must be a multiple of 64 for M > 16")
-    _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
+    _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, flags, ksplit,
               _p(aux), aux_rows, _p(aux_out), aux_ld, aux_n, _s())
     return out
 
@@ -80,6 +89,7 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
     """pg_gemm_fused: the GEMM with a fused prologue (x produced in-kernel) and/or RoPE/KV epilogue.
     `fa` is a PgFusedArgs (see fused_args); `keep` holds tensors it points to alive for the call."""
     _chk(W, torch.bfloat16, "W")
+    _chk_frag(W, epi)
     N = W.shape[0] if N is None else N
     K = W.shape[1]
     if ldc is None:
@@ -167,14 +177,6 @@ def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, ste
               _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
 
 
-def decode_mlp(**kw):
-    """pg_decode_mlp: persistent gate/up -> grid barrier -> down + finalisation (batch <= 2)."""
-    a = _lib.PgMlpArgs()
-    for k, v in kw.items():
-        setattr(a, k, v.data_ptr() if isinstance(v, torch.Tensor) else v)
-    _lib.call("pg_decode_mlp", _lib.C.byref(a), _s())
-
-
 def image_preprocess(src, H, W, S, hb, hk, hks, vb, vk, vks, y0, rows, lut, tmp, out):
     _chk(src, torch.uint8, "image")
     _chk(out, torch.float32, "pixel_values")
@@ -187,6 +189,14 @@ def synth_fill(out: torch.Tensor, seedmix: int, a: float, mean: float):
     if kind == 1:
         _chk(out, torch.float32, "out")
     _lib.call("pg_synth_fill", _p(out), out.numel(), seedmix & 0xFFFFFFFF, float(a), float(mean), kind, _s())
+
+
+def prefetch(t: torch.Tensor, wgs: int = 256, policy: int = 0, nbytes: Optional[int] = None):
+    """Read t's bytes (or its first nbytes) into the Infinity Cache ahead of the kernel that streams them."""
+    if not t.is_cuda:
+        raise RuntimeError("pghip: prefetch needs a HIP tensor")
+    n = t.numel() * t.element_size() if nbytes is None else nbytes
+    _lib.call("pg_prefetch", _p(t), n - n % 16, wgs, policy, _s())
 
 
 def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -> int:

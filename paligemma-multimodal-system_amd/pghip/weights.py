@@ -16,6 +16,11 @@ tensors of any float dtype on any device.  Output, on the HIP device:
 
 Padding rows/columns are zero so padded outputs are exactly 0 (gelu(0) = 0).
 
+The Gemma linear weights (q|k|v, o, gate/up, down and the lm_head copy of the embedding) are then
+stored fragment-packed (frag_pack; `frag` = True): the decode GEMVs stream them as 1 KiB lane-linear
+wave-instructions (gate/up 28.7 -> 23.0 us on MI355X) and the prefill tile GEMM stages them with the
+same per-lane address arithmetic.  The embedding used by the gather stays row-major.
+
 Tensor parallelism (tp_world > 1): rank r keeps the q heads
 [r*nh/W, (r+1)*nh/W) and every (replicated) k/v head, the matching o_proj input columns,
 the gate/up rows and down input columns of its slice [r*I/W, (r+1)*I/W) of the
@@ -30,6 +35,22 @@ import torch
 
 def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+def frag_pack(w: torch.Tensor) -> torch.Tensor:
+    """Row-major W[N][K] (N % 16 == 0, K % 64 == 0) -> the fragment-packed layout of include/pghip.h
+    PG_W_FRAG: W[16t + r][64c + 16g + 8s + e] at ((((t*K/64 + c)*2 + s)*64 + 16g + r)*8 + e), so that
+    every GEMV wave-instruction (lane 16g + r, piece s) reads 1 KiB contiguous.  Same shape [N][K]."""
+    N, K = w.shape
+    if N % 16 or K % 64:
+        raise ValueError(f"frag_pack needs N % 16 == 0 and K % 64 == 0, got {tuple(w.shape)}")
+    return w.reshape(N // 16, 16, K // 64, 4, 2, 8).permute(0, 2, 4, 3, 1, 5).contiguous().view(N, K)
+
+
+def frag_unpack(p: torch.Tensor) -> torch.Tensor:
+    """Inverse of frag_pack."""
+    N, K = p.shape
+    return p.reshape(N // 16, K // 64, 2, 4, 16, 8).permute(0, 4, 1, 3, 2, 5).contiguous().view(N, K)
 
 
 def rope_row_perm(D: int) -> torch.Tensor:
@@ -146,13 +167,19 @@ class PackedWeights:
         # tied lm_head rows of this rank's vocabulary slice (a view of the embedding when no padding is
         # needed; the GEMM wants N % 4 == 0, so an odd-sized slice gets a zero-padded copy)
         vo, vl = self.vocab_offset, self.vocab_local
-        self.vocab_local_pad = _rup(vl, 4)
         bias = f32(get(lm + "lm_head.bias"))[vo:vo + vl]
-        if self.vocab_local_pad == vl:
+        # every Gemma matrix must be packable (N % 16, K % 64), else all stay row-major (toy TP shards)
+        self.frag = (self.hidden % 64 == 0 and (self.heads * self.head_dim) % 64 == 0 and
+                     ((self.heads + 2 * self.kv_heads) * self.head_dim) % 16 == 0)
+        pad_to = 16 if self.frag else 4
+        self.vocab_local_pad = _rup(vl, pad_to)
+        if self.vocab_local_pad == vl and not self.frag:
             self.lm_w, self.lm_bias = self.embed[vo:vo + vl], bias.contiguous()
         else:
-            self.lm_w = torch.zeros(self.vocab_local_pad, self.hidden, dtype=torch.bfloat16, device=dev)
-            self.lm_w[:vl] = self.embed[vo:vo + vl]
+            lm_w = torch.zeros(self.vocab_local_pad, self.hidden, dtype=torch.bfloat16, device=dev)
+            lm_w[:vl] = self.embed[vo:vo + vl]
+            self.lm_w = frag_pack(lm_w) if self.frag else lm_w
+            del lm_w
             self.lm_bias = torch.zeros(self.vocab_local_pad, dtype=torch.float32, device=dev)
             self.lm_bias[:vl] = bias
         self.tl = []
@@ -169,13 +196,15 @@ class PackedWeights:
             gu = torch.stack([g.view(I // 16, 16, H), u.view(I // 16, 16, H)], dim=1).reshape(2 * I, H).contiguous()
             down = torch.zeros(H, I, dtype=torch.bfloat16, device=dev)
             down[:, :Ir] = bf(get(lp + "mlp.down_proj.weight")[:, i_lo:i_hi])
+            o_w = bf(get(a + "o_proj.weight")[:, q_lo:q_hi])
+            pk = frag_pack if self.frag else (lambda x: x)
             self.tl.append(dict(
-                in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=qkv_w,
-                o_w=bf(get(a + "o_proj.weight")[:, q_lo:q_hi]),
-                post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=gu,
-                down_w=down))
+                in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=pk(qkv_w), o_w=pk(o_w),
+                post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=pk(gu), down_w=pk(down)))
+            del qkv_w, o_w, gu, down
             del g, u
         self.final_w = f32(get(lm + "model.norm.weight"))
+        self.wflag = 0x100 if self.frag else 0            # ops.W_FRAG for every Gemma linear
         self.qkv_n = (self.heads + 2 * self.kv_heads) * hd
 
     def nbytes(self) -> int:

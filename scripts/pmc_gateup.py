@@ -17,6 +17,6 @@ w = weights.PackedWeights(cfg, sd.__getitem__, parts=("text",))
 x = torch.randn(1, w.hidden, device="cuda").to(torch.bfloat16)
 h = torch.empty(1, w.inter, dtype=torch.bfloat16, device="cuda")
 for i in range(36):
-    ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL)
+    ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
 torch.cuda.synchronize()
 print("launched 36 gate/up GEMVs")

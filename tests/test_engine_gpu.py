@@ -199,27 +199,3 @@ def test_batched_generation_per_row_eos(tiny, golden):
     for b in range(2):
         assert out[b, : len(single[b])].tolist() == single[b]
         assert (out[b, len(single[b]):] == 0).all()
-
-
-@pytest.mark.parametrize("persist", [True, False])
-def test_decode_layer_forms_agree(tiny, persist):
-    """The persistent MLP launch (gate/up -> grid barrier -> down + finalisation) against the
-    two-kernel form: same greedy tokens, logits within fp32 reassociation, no barrier give-up."""
-    eng, _ = tiny
-    g = np.load(__import__("os").path.join(__import__("conftest").GOLDEN, "tiny.npz"))
-    ids = torch.from_numpy(g["b1_input_ids"]).cuda()
-    px = torch.from_numpy(g["b1_pixel_values"]).cuda()
-    outs = []
-    for p in (persist, not persist):
-        eng.PERSIST_MLP = p
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 12)
-        st = eng.decode_state(1, cache, nxt, 12)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = []
-        for _ in range(10):
-            lg.append(eng.decode_step(st, cache, feats, dict(do_sample=False)).clone())
-        outs.append((st["hist"][:11, 0].tolist(), torch.stack(lg)))
-    eng.PERSIST_MLP = type(eng).PERSIST_MLP
-    assert outs[0][0] == outs[1][0]
-    assert err(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy()) < 1e-3
-    assert int(eng._ws["d_grid_err"][0]) == 0

@@ -125,3 +125,35 @@ def test_pil_bicubic_restatement_is_bit_exact(H, W, S):
     assert np.array_equal(resize_u8(img, S, resample_coeffs), ref)
     x = (np.arange(256, dtype=np.uint8) * (1 / 255.0)).astype(np.float32)
     assert np.array_equal(normalise_lut(), (x - np.float32(0.5)) / np.float32(0.5))
+
+
+def test_frag_pack_layout_and_roundtrip():
+    """weights.frag_pack puts W[16t+r][64c+16g+8s+e] at ((((t*K/64+c)*2+s)*64+16g+r)*8+e) (include/pghip.h
+    PG_W_FRAG) and frag_unpack inverts it."""
+    from pghip.weights import frag_pack, frag_unpack
+    N, K = 48, 192
+    w = torch.arange(N * K, dtype=torch.int64).reshape(N, K)
+    p = frag_pack(w).reshape(-1)
+    for (n, k) in [(0, 0), (17, 65), (47, 191), (31, 100), (5, 24)]:
+        t, r, c, kk = n // 16, n % 16, k // 64, k % 64
+        g, s, e = kk // 16, (kk % 16) // 8, kk % 8
+        assert int(p[(((t * (K // 64) + c) * 2 + s) * 64 + 16 * g + r) * 8 + e]) == n * K + k
+    assert torch.equal(frag_unpack(frag_pack(w)), w)
+    with pytest.raises(ValueError):
+        frag_pack(torch.zeros(40, 128))
+
+
+def test_packed_weights_frag_flags():
+    """Gemma matrices fragment-packed when every shape allows it (full size, tiny), row-major for toy TP shards."""
+    from pghip.weights import PackedWeights, frag_unpack, rope_row_perm
+    cfg = ocfg.TINY
+    W = synth.generate_state_dict(cfg)
+    P = PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu", parts=("text",))
+    assert P.frag and P.wflag == 0x100 and P.vocab_local_pad % 16 == 0
+    down = frag_unpack(P.tl[0]["down_w"]).float().numpy()
+    want = W["language_model.model.layers.0.mlp.down_proj.weight"]
+    assert np.array_equal(down[:, :want.shape[1]], want.astype(np.float32))
+    lm = frag_unpack(P.lm_w).float().numpy()[:cfg["text_config"]["vocab_size"]]
+    assert np.array_equal(lm, W["language_model.model.embed_tokens.weight"].astype(np.float32))
+    P4 = PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu", parts=("text",), tp_rank=1, tp_world=4)
+    assert not P4.frag and P4.wflag == 0

@@ -84,6 +84,27 @@ def test_gemm_gelu_and_gelu_mul(M):
     assert err(out2, torch.nn.functional.gelu(A.float() @ g.float().t() + bias, approximate="tanh")) < 1e-2
 
 
+@pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 264])
+@pytest.mark.parametrize("N,K", [(256, 128), (2048, 2048), (320, 1024)])
+def test_gemm_frag_packed_weights_bit_identical(M, N, K):
+    """W_FRAG (fragment-packed W, the Gemma HBM layout) feeds the GEMV and the tile GEMM exactly the
+    values the row-major layout does: outputs are bit-identical, for every Gemma epilogue."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    A, W = rnd(M, K, seed=21), rnd(N, K, scale=1 / math.sqrt(K), seed=22)
+    Wp = frag_pack(W)
+    bias = torch.randn(N).cuda()
+    for epi, dt, ks in ((ops.EPI_BF16, torch.bfloat16, 1), (ops.EPI_F32, torch.float32, 1),
+                        (ops.EPI_F32, torch.float32, 4), (ops.EPI_BF16_GELU_MUL, torch.bfloat16, 1)):
+        n_out = N // 2 if epi == ops.EPI_BF16_GELU_MUL else N
+        shape = (ks, M, n_out) if epi == ops.EPI_F32 else (M, n_out)
+        a, b = torch.empty(shape, dtype=dt, device="cuda"), torch.empty(shape, dtype=dt, device="cuda")
+        bb = None if epi == ops.EPI_BF16_GELU_MUL else bias
+        ops.gemm(A, W, a, epi=epi, bias=bb, ksplit=ks)
+        ops.gemm(A, Wp, b, epi=epi | ops.W_FRAG, bias=bb, ksplit=ks)
+        assert torch.equal(a, b), (epi, ks)
+
+
 def test_gemm_vt_and_pos_epilogues():
     from pghip import ops
     M, K, hv = 40, 192, 64

@@ -25,8 +25,8 @@ def _free_port() -> int:
 
 def _unpack_layer(P, i):
     """Packed (kernel-layout) slices of layer i back to reference-layout weights of this shard."""
-    from pghip.weights import rope_row_perm
-    L = P.tl[i]
+    from pghip.weights import frag_unpack, rope_row_perm
+    L = {k: (frag_unpack(v) if P.frag and v.dim() == 2 else v) for k, v in P.tl[i].items()}
     hd, H, nb = P.head_dim, P.hidden, P.heads + 2 * P.kv_heads
     inv = torch.argsort(rope_row_perm(hd))
     qkv = L["qkv_w"].float().view(nb, hd, H)[:, inv, :]
@@ -74,7 +74,9 @@ def _worker(rank, world, port, cfg_name):
         # vocabulary-parallel lm_head: each rank fills its slot of a zeroed buffer, SUM all-reduce gathers
         xr = x.reshape(-1, H)
         g = torch.zeros(xr.shape[0], world, P.vocab_local_pad)
-        g[:, rank] = torch.from_numpy(xr) @ P.lm_w.float().T + P.lm_bias
+        from pghip.weights import frag_unpack
+        lm_w = frag_unpack(P.lm_w) if P.frag else P.lm_w
+        g[:, rank] = torch.from_numpy(xr) @ lm_w.float().T + P.lm_bias
         dist.all_reduce(g)
         full = xr @ W["language_model.model.embed_tokens.weight"].T + W["language_model.lm_head.bias"]
         np.testing.assert_allclose(g[:, :, :P.vocab_local].reshape(xr.shape[0], -1).numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
