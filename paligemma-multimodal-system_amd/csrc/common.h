@@ -6,6 +6,7 @@
 typedef uint16_t bf16_t;                                       // bf16 storage
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;     // MFMA A/B fragment (4 VGPRs)
 typedef __attribute__((ext_vector_type(4))) float f32x4;       // 16x16 accumulator fragment
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;    // 16-byte raw load
 typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;    // 8-byte raw load
 

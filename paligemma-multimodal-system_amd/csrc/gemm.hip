@@ -380,6 +380,12 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
 #endif
+#ifndef PG_T_NOMERGE
+#define PG_T_NOMERGE 0
+#endif
+#ifndef PG_T_NOFIN
+#define PG_T_NOFIN 0
+#endif
 #ifndef PG_GEMV_D2
 #define PG_GEMV_D2 4
 #endif
@@ -496,7 +502,46 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
     const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
     const int Seff = (f.slot_dev && f.akeys > 0) ? min(S, (*f.slot_dev + f.akeys) / f.akeys) : S;
     const int h0 = k0 / D, nh = Kr / D, D4 = D >> 2;
-    const int items = M * nh * D4;
+    const int items = PG_T_NOMERGE ? 0 : M * nh * D4;   // PG_T_NOMERGE: timing experiment only (x = 0)
+    if (PG_T_NOMERGE)
+      for (int idx = t; idx < M * Kr / 4; idx += 256) *(u32x2*)(xs + (idx / (Kr / 4)) * ldx + (idx % (Kr / 4)) * 4) = u32x2{0u, 0u};
+    if (S <= 16 && !PG_T_NOMERGE) {
+      // every split's (m, l, o) loaded at once (one dependent L2 round trip, no read of the kv length:
+      // splits past it hold m = -inf and weigh 0), then a two-pass max / weighted sum
+      for (int idx = t; idx < M * nh * D4; idx += 256) {
+        const int m = idx / (nh * D4), rem = idx % (nh * D4), hl = rem / D4, d4 = rem % D4;
+        const int hq = h0 + hl;
+        const long base0 = (((long)m * f.kv_heads + hq / G) * S) * 16 + (hq % G);
+        float ms[16], ls[16];
+        f32x4 o4[16];
+#pragma unroll
+        for (int sp = 0; sp < 16; ++sp) {
+          const long bs = base0 + (long)min(sp, S - 1) * 16;
+          const f32x2 v = *(const f32x2*)(f.part_ml + bs * 2);
+          ms[sp] = sp < S ? v[0] : -INFINITY;
+          ls[sp] = v[1];
+          o4[sp] = *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+        }
+        float mx = ms[0];
+#pragma unroll
+        for (int sp = 1; sp < 16; ++sp) mx = fmaxf(mx, ms[sp]);
+        float den = 0.f;
+        f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sp = 0; sp < 16; ++sp) {
+          const float w = ms[sp] == -INFINITY ? 0.f : exp2f(ms[sp] - mx);
+          den += w * ls[sp];
+          num += w * o4[sp];
+        }
+        const float inv = 1.0f / den;
+        u32x2 pk;
+        pk[0] = pack_bf2(num[0] * inv, num[1] * inv);
+        pk[1] = pack_bf2(num[2] * inv, num[3] * inv);
+        *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
+      }
+      __syncthreads();
+      return;
+    }
     for (int idx = t; idx < items; idx += 256) {
       const int m = idx / (nh * D4), rem = idx % (nh * D4), hl = rem / D4, d4 = rem % D4;
       const int hq = h0 + hl;
@@ -747,6 +792,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (PG_T_NOFIN) return;                                  // timing experiment only: slabs never reduced
     int old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(f.fin_cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0, 64);
