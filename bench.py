@@ -265,6 +265,7 @@ def main():
     ev[1].record()
     state["st"]["kv_len"].fill_(L)
     state["st"]["pos"].fill_(L + 1)
+    state["st"]["step"].zero_()
     ev[2].record()
     for _ in range(T - 1):
         replay()

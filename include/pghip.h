@@ -128,21 +128,23 @@ int pg_embed_merge(const int64_t* ids, const int* rank, int n, const void* embed
                    int n_feat, int H, long image_id, long pad_id, float img_scale, float normalizer,
                    float* out, hipStream_t stream);
 
-/* greedy next token (inference.py:59,68), first index on ties; optional decode-state advance. */
+/* greedy next token (inference.py:59,68), first index on ties; optional decode-state advance:
+ * hist[*step][b] = token (only while *step < hist_rows), pos[b] += 1, *kv_len += 1, *step += 1. */
 int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
-              int64_t* hist, int* step, int* pos, int* kv_len, hipStream_t stream);
+              int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, hipStream_t stream);
 
 /* vocabulary-parallel greedy for tensor parallelism: local (max, first global index) pairs [B][2] of a
  * vocab shard starting at vocab_offset; after an all-gather, pg_argmax_merge takes the global winner
  * (lowest index on ties, as torch.argmax) and advances the decode state like pg_argmax. */
 int pg_argmax_pairs(const float* logits, long ld, int B, int V, int vocab_offset, void* workspace,
                     float* pairs, hipStream_t stream);
-int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int* step,
-                    int* pos, int* kv_len, hipStream_t stream);
+int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int hist_rows,
+                    int* step, int* pos, int* kv_len, hipStream_t stream);
 
-/* softmax(logits/T) + top-p filter (inference.py:65,90-102) + explicit-uniform inverse-CDF draw. */
+/* softmax(logits/T) + top-p filter (inference.py:65,90-102) + explicit-uniform inverse-CDF draw.
+ * uniforms [hist_rows][B] indexed by min(*step, hist_rows - 1); hist as pg_argmax. */
 int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature, float top_p,
-                   const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
+                   const float* uniforms, int64_t* out_ids, int64_t* hist, int hist_rows, int* step, int* pos,
                    int* kv_len, float* probs_out, hipStream_t stream);
 
 /* Reference image pre-processing (processing_paligemma.py:13-73) on the device: PIL BICUBIC resize of an RGB

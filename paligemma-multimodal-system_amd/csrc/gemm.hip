@@ -114,6 +114,7 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
   const int d0 = second ? half + ii : ii;             // original dim of element 0
   const int b = m / f.rows_per_batch, i = m % f.rows_per_batch;
   const int slot = f.slot_base + (f.slot_dev ? *f.slot_dev : 0) + i;
+  const bool in_cache = slot < f.smax;                // a token past the static cache is not appended
   const int Hq = f.q_heads, Hkv = f.kv_heads;
   const int KV = Hkv * D;
   if (blk < Hq + Hkv) {
@@ -131,10 +132,10 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
     pk[1] = pack_bf2(y[2], y[3]);
     if (blk < Hq) {
       *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0) = pk;
-    } else {
+    } else if (in_cache) {
       *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
     }
-  } else {
+  } else if (in_cache) {
     const int c0 = (blk - Hq - Hkv) * D + d0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
@@ -351,6 +352,153 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 }
 
 // --------------------------------------------------------------------------------------
+// Large-M GEMM (prefill at batch x image tokens >= a few thousand rows): 256 x 256 x 64 tiles
+// --------------------------------------------------------------------------------------
+// 8 waves = 2 (M) x 4 (N), each owning 128 x 64 outputs (acc[8][4] 16x16 fragments), one workgroup per
+// CU (128 KiB LDS).  A K-tile is staged as four 16 KiB half-images (128 rows x 128 B, XOR-swizzled through
+// the source address, global_load_lds 16 B/lane, 2 per thread):
+//   A0 = tile rows {0..63, 128..191}   A1 = rows {64..127, 192..255}      (wave rows wr*128 + [0,64) / [64,128))
+//   B0 = W rows {64c + [0,32)}         B1 = W rows {64c + [32,64)}, c < 4 (wave columns wc*64 + [0,32) / [32,64))
+// and consumed in four phases, one C quadrant each: (A0,B0) (A0 regs,B1) (A1,B1 regs) (A1,B0).  A half is
+// restaged one phase after its last read (A0 of tile t+2 in phase 1 of t, B1 in phase 2, A1 in phase 3,
+// B0 of t+1 in phase 0), so 3 half-tiles (6 loads per thread) stay in flight across the raw s_barrier that
+// ends every phase; the single counted wait (vmcnt 6) sits in phase 3 and the tile it retires is read
+// from phase 0 of the next tile on (MI355X guide: 256^2 8-phase template, counted vmcnt, T1/T2/T5).
+template <int EPI, bool FRAG>
+__global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
+                                                      const bf16_t* __restrict__ W, int ldw, int K,
+                                                      int tiles_m, int tiles_n, EpiArgs e) {
+  constexpr int HALF = 16384;
+  __shared__ __attribute__((aligned(1024))) char smem[8 * HALF];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = gridDim.x;
+  int pid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = pid & 7, idx = pid >> 3;
+    pid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  const int GROUP = 8;
+  const int group = pid / (GROUP * tiles_n);
+  const int first_m = group * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int tm = first_m + (pid % gsize);
+  const int tn = (pid % (GROUP * tiles_n)) / gsize;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = K / 64;
+
+  auto stage = [&](int h, int kt) {
+    char* dst = smem + ((kt & 1) * 4 + h) * HALF;
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int blk = wave * 2 + it;                 // 16 pieces of 8 rows x 128 B
+      const int r = blk * 8 + (lane >> 3);           // half-image row
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const bf16_t* src;
+      if (h < 2) {
+        const int gr = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), e.M - 1);
+        src = A + (size_t)gr * lda + k0 + c * 8;
+      } else {
+        const int gn = min(n0 + (r >> 5) * 64 + (h - 2) * 32 + (r & 31), e.N - 1);
+        src = FRAG ? W + frag_off(gn, k0, c, ldw) : W + (size_t)gn * ldw + k0 + c * 8;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + blk * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb[2][2];
+
+  auto read_a = [&](const char* img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(img, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
+  };
+  auto read_b = [&](const char* img) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) fb[j][s] = lds_frag(img, wc * 32 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+  };
+  auto mma = [&](int rh, int ch) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[rh * 4 + i][ch * 2 + j] = mfma16(fb[j][s], fa[i][s], acc[rh * 4 + i][ch * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: all of tile 0, then the three halves of tile 1 that phases 1-3 of tile -1 would have issued
+#pragma unroll
+  for (int h = 0; h < 4; ++h) stage(h, 0);
+  if (nk > 1) {
+    stage(0, 1);
+    stage(3, 1);
+    stage(1, 1);
+    wait_vm(6);
+  } else {
+    wait_vm(0);
+  }
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * 4 * HALF;
+    // phase 0: quadrant (rows 0-63, cols 0-31) from A0, B0; restage B0 of tile t+1
+    read_a(buf);
+    read_b(buf + 2 * HALF);
+    if (t + 1 < nk) stage(2, t + 1);
+    mma(0, 0);
+    __builtin_amdgcn_s_barrier();
+    // phase 1: (rows 0-63, cols 32-63) A regs kept, B1; restage A0 of tile t+2 (A0 was last read in phase 0)
+    read_b(buf + 3 * HALF);
+    if (t + 2 < nk) stage(0, t + 2);
+    mma(0, 1);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: (rows 64-127, cols 32-63) A1, B regs kept; restage B1 of tile t+2
+    read_a(buf + 1 * HALF);
+    if (t + 2 < nk) stage(3, t + 2);
+    mma(1, 1);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: (rows 64-127, cols 0-31) A regs kept, B0 again; restage A1 of tile t+2; retire tile t+1
+    read_b(buf + 2 * HALF);
+    if (t + 2 < nk) stage(1, t + 2);
+    mma(1, 0);
+    if (t + 2 < nk) wait_vm(6); else wait_vm(0);
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // epilogue: acc[i][j] lane holds C[m][n..n+3], m = m0 + wr*128 + (i/4)*64 + (i%4)*16 + (lane&15),
+  // n = n0 + wc*64 + (j/2)*32 + (j%2)*16 + 4*(lane>>4)
+  const int q = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16;
+      if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+        if ((j & 1) == 0) epi_gelu_mul4(e, m, nb, q, acc[i][j], acc[i][j + 1]);
+      } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+        epi_qkv_rope4(e, m, nb + q, acc[i][j]);
+      } else {
+        epi_store4<EPI>(e, m, nb + q, acc[i][j], 0);
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // Skinny GEMM / GEMV (M <= 16): weight streaming straight to VGPRs
 // --------------------------------------------------------------------------------------
 // One workgroup = 4 waves on NT adjacent 16-row tiles of W (NT = 2 for the interleaved gate/up
@@ -379,6 +527,9 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #endif
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
+#endif
+#ifndef PG_G256_MIN_TILES
+#define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
 #endif
 #ifndef PG_T_NOMERGE
 #define PG_T_NOMERGE 0
@@ -857,6 +1008,12 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 template <int EPI, bool FRAG>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
+  const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
+  if (ksplit == 1 && t256 >= PG_G256_MIN_TILES) {
+    hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG>), dim3(t256), dim3(512), 0, st, A, lda, W, ldw, K,
+                       (e.M + 255) / 256, (e.N + 255) / 256, e);
+    return;
+  }
   const int tiles_n = (e.N + TBN - 1) / TBN;
   int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
   const int t128 = ((e.M + 127) / 128) * tiles_n;

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void argmax_partial_kernel(const float* __rest
 //   out_ids[b] = argmax ; hist[(*step) * B + b] = argmax ; pos[b] += 1 ; (*kv_len) += 1 ; (*step) += 1
 __global__ __launch_bounds__(64) void argmax_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
                                                           int B, int64_t* __restrict__ out_ids, int64_t* __restrict__ hist,
-                                                          int* __restrict__ step, int* __restrict__ pos,
+                                                          int hist_rows, int* __restrict__ step, int* __restrict__ pos,
                                                           int* __restrict__ kv_len) {
   const int lane = threadIdx.x;
   const int st = step ? *step : 0;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(64) void argmax_final_kernel(const float* __restric
     }
     if (lane == 0) {
       out_ids[b] = bi;
-      if (hist) hist[(long)st * B + b] = bi;
+      if (hist && st < hist_rows) hist[(long)st * B + b] = bi;   // a step past the history is not recorded
       if (pos) pos[b] += 1;
     }
   }
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64) void argmax_pairs_kernel(const float* __restric
 
 // pairs [world][B][2] (rank-major, ascending vocabulary ranges): max value, lowest global index on ties
 __global__ void argmax_merge_kernel(const float* __restrict__ pairs, int world, int B, int64_t* __restrict__ out_ids,
-                                    int64_t* __restrict__ hist, int* __restrict__ step, int* __restrict__ pos,
+                                    int64_t* __restrict__ hist, int hist_rows, int* __restrict__ step, int* __restrict__ pos,
                                     int* __restrict__ kv_len) {
   if (threadIdx.x != 0) return;
   const int st = step ? *step : 0;
@@ -280,7 +280,7 @@ __global__ void argmax_merge_kernel(const float* __restrict__ pairs, int world, 
     int bi = 0x7FFFFFFF;
     for (int r = 0; r < world; ++r) am_better(bv, bi, pairs[(r * B + b) * 2], (int)pairs[(r * B + b) * 2 + 1]);
     out_ids[b] = bi;
-    if (hist) hist[(long)st * B + b] = bi;
+    if (hist && st < hist_rows) hist[(long)st * B + b] = bi;
     if (pos) pos[b] += 1;
   }
   if (kv_len) *kv_len += 1;
@@ -298,23 +298,24 @@ extern "C" int pg_argmax_pairs(const float* logits, long ld, int B, int V, int v
   return 0;
 }
 
-extern "C" int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int* step,
-                               int* pos, int* kv_len, hipStream_t stream) {
-  PG_REQUIRE(world > 0 && B > 0);
-  hipLaunchKernelGGL(argmax_merge_kernel, dim3(1), dim3(64), 0, stream, pairs, world, B, out_ids, hist, step, pos,
-                     kv_len);
+extern "C" int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int hist_rows,
+                               int* step, int* pos, int* kv_len, hipStream_t stream) {
+  PG_REQUIRE(world > 0 && B > 0 && (hist == nullptr || hist_rows > 0));
+  hipLaunchKernelGGL(argmax_merge_kernel, dim3(1), dim3(64), 0, stream, pairs, world, B, out_ids, hist, hist_rows,
+                     step, pos, kv_len);
   PG_LAUNCH_CHECK();
   return 0;
 }
 
 // workspace: >= B * AM_CHUNKS * 8 bytes
 extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
-                         int64_t* hist, int* step, int* pos, int* kv_len, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && V > 0 && ld % 4 == 0);
+                         int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, hipStream_t stream) {
+  PG_REQUIRE(B > 0 && V > 0 && ld % 4 == 0 && (hist == nullptr || hist_rows > 0));
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
-  hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(64), 0, stream, pv, pi, B, out_ids, hist, step, pos, kv_len);
+  hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(64), 0, stream, pv, pi, B, out_ids, hist, hist_rows, step, pos,
+                     kv_len);
   PG_LAUNCH_CHECK();
   return 0;
 }
@@ -327,7 +328,7 @@ extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* works
 // in vocabulary order over the included, renormalised mass: first i with prefix > u * Z_kept.
 __global__ __launch_bounds__(1024) void topp_kernel(const float* __restrict__ logits, long ld, int V, float inv_temp,
                                                     float top_p, const float* __restrict__ uniforms,
-                                                    int64_t* __restrict__ out_ids, int64_t* __restrict__ hist,
+                                                    int64_t* __restrict__ out_ids, int64_t* __restrict__ hist, int hist_rows,
                                                     int* __restrict__ step, int* __restrict__ pos, int B,
                                                     int* __restrict__ kv_len, float* __restrict__ probs_out) {
   __shared__ float red[16];
@@ -411,7 +412,9 @@ __global__ __launch_bounds__(1024) void topp_kernel(const float* __restrict__ lo
       probs_out[(long)b * V + i] = v >= t0 ? v / kept : 0.f;
     }
   }
-  const float u = uniforms[(step ? (long)(*step) * B : 0) + b] * kept;
+  // uniforms and hist hold hist_rows steps: a step past them reuses the last row / is not recorded
+  const long srow = step ? (long)min(*step, hist_rows - 1) : 0;
+  const float u = uniforms[srow * B + b] * kept;
   const float lo = scan[tid] - mine;
   __shared__ int chosen;
   if (tid == 0) chosen = -1;
@@ -436,7 +439,7 @@ __global__ __launch_bounds__(1024) void topp_kernel(const float* __restrict__ lo
       for (int i = V - 1; i >= 0; --i) if (__expf(x[i] * inv_temp - mx) >= t0) { c = i; break; }
     }
     out_ids[b] = c;
-    if (hist) hist[(step ? (long)(*step) * B : 0) + b] = c;
+    if (hist && (!step || *step < hist_rows)) hist[srow * B + b] = c;
     if (pos) pos[b] += 1;
   }
 }
@@ -449,11 +452,11 @@ __global__ void advance_kernel(int* step, int* kv_len) {
 // uniforms: [steps][B] (indexed by *step when step != null).  probs_out (optional) f32 [B][V]: the filtered,
 // renormalised distribution in vocabulary order (for tests).
 extern "C" int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature, float top_p,
-                              const float* uniforms, int64_t* out_ids, int64_t* hist, int* step, int* pos,
+                              const float* uniforms, int64_t* out_ids, int64_t* hist, int hist_rows, int* step, int* pos,
                               int* kv_len, float* probs_out, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && V > 0 && temperature > 0.f);
+  PG_REQUIRE(B > 0 && V > 0 && temperature > 0.f && hist_rows > 0);
   hipLaunchKernelGGL(topp_kernel, dim3(B), dim3(1024), 0, stream, logits, ld, V, 1.0f / temperature, top_p, uniforms,
-                     out_ids, hist, step, pos, B, kv_len, probs_out);
+                     out_ids, hist, hist_rows, step, pos, B, kv_len, probs_out);
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, stream, step, kv_len);
   PG_LAUNCH_CHECK();
   return 0;

@@ -41,10 +41,10 @@ SIGNATURES = {
     "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],
     "pg_image_rank": [vp, i32, i64, vp, vp],
     "pg_embed_merge": [vp, vp, i32, vp, i32, vp, i32, i32, i64, i64, f32, f32, vp, vp],
-    "pg_argmax": [vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp],
+    "pg_argmax": [vp, i64, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp],
     "pg_argmax_pairs": [vp, i64, i32, i32, i32, vp, vp, vp],
-    "pg_argmax_merge": [vp, i32, i32, vp, vp, vp, vp, vp, vp],
-    "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp],
+    "pg_argmax_merge": [vp, i32, i32, vp, vp, i32, vp, vp, vp, vp],
+    "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
     "pg_prefetch": [vp, i64, i32, i32, vp],

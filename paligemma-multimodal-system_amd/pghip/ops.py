@@ -151,11 +151,16 @@ def embed_merge(ids, rank, embed, feat, n_feat, out, *, image_id, pad_id, img_sc
               int(pad_id), float(img_scale), float(normalizer), _p(out), _s())
 
 
+def _rows(t: Optional[torch.Tensor], B: int) -> int:
+    """Steps a [steps][B] decode-state buffer holds (its step-indexed writes/reads are bounded by this)."""
+    return 0 if t is None else t.numel() // B
+
+
 def argmax(logits, out_ids, workspace, *, hist=None, step=None, pos=None, kv_len=None):
     _chk(logits, torch.float32, "logits")
     B, V = logits.shape
-    _lib.call("pg_argmax", _p(logits), logits.stride(0), B, V, _p(workspace), _p(out_ids), _p(hist), _p(step),
-              _p(pos), _p(kv_len), _s())
+    _lib.call("pg_argmax", _p(logits), logits.stride(0), B, V, _p(workspace), _p(out_ids), _p(hist), _rows(hist, B),
+              _p(step), _p(pos), _p(kv_len), _s())
 
 
 def argmax_pairs(logits, workspace, pairs, *, vocab_offset: int):
@@ -166,15 +171,17 @@ def argmax_pairs(logits, workspace, pairs, *, vocab_offset: int):
 
 def argmax_merge(pairs, out_ids, *, world: int, hist=None, step=None, pos=None, kv_len=None):
     B = out_ids.numel()
-    _lib.call("pg_argmax_merge", _p(pairs), int(world), B, _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _s())
+    _lib.call("pg_argmax_merge", _p(pairs), int(world), B, _p(out_ids), _p(hist), _rows(hist, B), _p(step), _p(pos),
+              _p(kv_len), _s())
 
 
 def topp_sample(logits, out_ids, uniforms, *, temperature, top_p, hist=None, step=None, pos=None, kv_len=None,
                 probs_out=None):
     _chk(logits, torch.float32, "logits")
     B, V = logits.shape
+    rows = _rows(uniforms, B) if hist is None else min(_rows(uniforms, B), _rows(hist, B))
     _lib.call("pg_topp_sample", _p(logits), logits.stride(0), B, V, float(temperature), float(top_p), _p(uniforms),
-              _p(out_ids), _p(hist), _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
+              _p(out_ids), _p(hist), rows, _p(step), _p(pos), _p(kv_len), _p(probs_out), _s())
 
 
 def image_preprocess(src, H, W, S, hb, hk, hks, vb, vk, vks, y0, rows, lut, tmp, out):

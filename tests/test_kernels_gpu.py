@@ -278,6 +278,11 @@ def test_argmax_first_index_and_state_advance():
     assert ids.cpu().tolist() == want.tolist() and ids[1].item() == 77
     assert hist[2].cpu().tolist() == want.tolist()
     assert step.item() == 3 and kv.item() == 10 and pos.cpu().tolist() == [6, 7, 8]
+    # a step past the history's rows is not recorded (the state still advances)
+    guard = torch.full((6, 3), -7, dtype=torch.int64, device="cuda")
+    step.fill_(4)
+    ops.argmax(x, ids, ws, hist=guard[:4], step=step, pos=pos, kv_len=kv)
+    assert (guard[4:] == -7).all() and step.item() == 5 and ids.cpu().tolist() == want.tolist()
 
 
 def test_topp_matches_reference_filter(golden):
@@ -402,3 +407,29 @@ def test_image_preprocess_bit_exact_with_reference_host_path(H, W, S):
     out = image.preprocess([img], S)
     assert out.shape == (1, 3, S, S) and out.dtype == torch.float32
     assert np.array_equal(out[0].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(4200, 4096, 640), (16384, 1152, 1152), (2100, 8192, 256), (4113, 4096, 192)])
+def test_gemm256_large_m(M, N, K):
+    """The 256x256 large-M GEMM (chosen when its grid fills every CU), ragged M/N edges, odd K-tile counts,
+    row-major and fragment-packed W, against a torch fp32 matmul of the same bf16 operands."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    A, W = rnd(M, K, seed=31), rnd(N, K, scale=1 / math.sqrt(K), seed=32)
+    bias = torch.randn(N).cuda()
+    ref = A.float() @ W.float().t() + bias
+    out = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    ops.gemm(A, W, out, epi=ops.EPI_F32, bias=bias)
+    assert err(out, ref) < 1e-5
+    outb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    if N % 16 == 0 and K % 64 == 0:
+        ops.gemm(A, frag_pack(W), outb, epi=ops.EPI_BF16 | ops.W_FRAG, bias=bias)
+    else:
+        ops.gemm(A, W, outb, bias=bias)
+    assert err(outb, ref) < 1e-2
+    if N % 32 == 0:
+        h = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
+        ops.gemm(A, W, h, epi=ops.EPI_BF16_GELU_MUL)
+        g = (A.float() @ W.float().t()).view(M, N // 32, 2, 16)
+        want = (torch.nn.functional.gelu(g[:, :, 0], approximate="tanh") * g[:, :, 1]).reshape(M, N // 2)
+        assert err(h, want) < 1e-2
