@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 template <int EPI, bool FRAG>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, int K,
-                                                      int tiles_m, int tiles_n, EpiArgs e) {
+                                                      int ktiles_per_split, int tiles_m, int tiles_n, EpiArgs e) {
   constexpr int HALF = 16384;
   __shared__ __attribute__((aligned(1024))) char smem[8 * HALF];
   const int lane = threadIdx.x & 63;
@@ -387,11 +387,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   const int tm = first_m + (pid % gsize);
   const int tn = (pid % (GROUP * tiles_n)) / gsize;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int nk = K / 64;
+  // split-K (fp32 partial epilogue only): slice z covers k-tiles [kt0, kt0 + nk)
+  const int z = blockIdx.z;
+  const int kt0 = z * ktiles_per_split;
+  const int nk = max(0, min(K / 64 - kt0, ktiles_per_split));
 
   auto stage = [&](int h, int kt) {
     char* dst = smem + ((kt & 1) * 4 + h) * HALF;
-    const int k0 = kt * 64;
+    const int k0 = (kt0 + kt) * 64;
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int blk = wave * 2 + it;                 // 16 pieces of 8 rows x 128 B
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
       } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
         epi_qkv_rope4(e, m, nb + q, acc[i][j]);
       } else {
-        epi_store4<EPI>(e, m, nb + q, acc[i][j], 0);
+        epi_store4<EPI>(e, m, nb + q, acc[i][j], z);
       }
     }
   }
@@ -1009,8 +1012,9 @@ template <int EPI, bool FRAG>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
-  if (ksplit == 1 && t256 >= PG_G256_MIN_TILES) {
-    hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG>), dim3(t256), dim3(512), 0, st, A, lda, W, ldw, K,
+  if (t256 >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
+    const int kts = (K / 64 + ksplit - 1) / ksplit;
+    hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
                        (e.M + 255) / 256, (e.N + 255) / 256, e);
     return;
   }

@@ -128,9 +128,8 @@ class PaliGemmaEngine:
         vt = self._buf("v_vt", (hv, M + 32), torch.bfloat16)            # rows padded: attention reads 32-key blocks
         attn = self._buf("v_attn", (M, hv), torch.bfloat16)
         h = self._buf("v_h", (M, w.v_inter), torch.bfloat16)
-        tiles = lambda n: ((M + 63) // 64) * ((n + 127) // 128)  # noqa: E731
-        s_o = ops.split_for(tiles(hv), hv // 64)
-        s_2 = ops.split_for(tiles(hv), w.v_inter // 64)
+        s_o = ops.gemm_ksplit(M, hv, hv)
+        s_2 = ops.gemm_ksplit(M, hv, w.v_inter)
         part = self._buf("v_part", (max(s_o, s_2), M, hv), torch.float32)
         ns = 0
         for L in w.vl:
@@ -182,9 +181,8 @@ class PaliGemmaEngine:
         qb = self._buf("t_q", (T, nh * hd), torch.bfloat16)
         attn = self._buf("t_attn", (T, nh * hd), torch.bfloat16)
         h = self._buf("t_h", (T, I), torch.bfloat16)
-        tiles = lambda n: ((T + 63) // 64) * ((n + 127) // 128)  # noqa: E731
-        s_o = ops.split_for(tiles(H), (nh * hd) // 64) if T > 16 else self.DECODE_SPLIT_O
-        s_d = ops.split_for(tiles(H), I // 64) if T > 16 else self.DECODE_SPLIT_DOWN
+        s_o = ops.gemm_ksplit(T, H, nh * hd) if T > 16 else self.DECODE_SPLIT_O
+        s_d = ops.gemm_ksplit(T, H, I) if T > 16 else self.DECODE_SPLIT_DOWN
         part = self._buf("t_part", (max(s_o, s_d), T, H), torch.float32)
         pos = positions.to(device=self.device, dtype=torch.int32).reshape(-1).contiguous()
         ns = 0

@@ -210,3 +210,27 @@ def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -
     """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
     s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))
     return s
+
+
+CUS = 256   # MI355X compute units
+
+
+def gemm_ksplit(M: int, N: int, K: int) -> int:
+    """split-K factor for an fp32-partial (EPI_F32) prefill GEMM, mirroring libpghip's tile choice.
+    Large M (a 256x256 grid of >= 256 tiles, csrc/gemm.hip gemm256_kernel): the split that best fills the
+    last round of one-workgroup-per-CU tiles, each extra split charged its partial-slab round trip
+    (2*M*N*4 B at ~5 TB/s against 2*M*N*K flop at ~1 PF/s, i.e. 800/K of the GEMM per split).
+    Smaller M: enough 64x128 tiles x splits to reach every CU (split_for)."""
+    t256 = math.ceil(M / 256) * math.ceil(N / 256)
+    if t256 >= CUS:
+        kt = K // 64
+        best, best_s = -1.0, 1
+        for s in (1, 2, 3, 4):
+            if s > 1 and kt // s < 8:
+                break
+            u = t256 * s
+            eff = u / (math.ceil(u / CUS) * CUS) - 800.0 / K * (s - 1)
+            if eff > best + 1e-9:
+                best, best_s = eff, s
+        return best_s
+    return split_for(math.ceil(M / 64) * math.ceil(N / 128), K // 64)

@@ -421,6 +421,10 @@ def test_gemm256_large_m(M, N, K):
     out = torch.empty(M, N, dtype=torch.float32, device="cuda")
     ops.gemm(A, W, out, epi=ops.EPI_F32, bias=bias)
     assert err(out, ref) < 1e-5
+    for ks in (2, 3):   # split-K fp32 slabs (bias on slab 0), ragged last slice
+        part = torch.empty(ks, M, N, dtype=torch.float32, device="cuda")
+        ops.gemm(A, W, part, epi=ops.EPI_F32, bias=bias, ksplit=ks)
+        assert err(part.sum(0), ref) < 1e-5, ks
     outb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     if N % 16 == 0 and K % 64 == 0:
         ops.gemm(A, frag_pack(W), outb, epi=ops.EPI_BF16 | ops.W_FRAG, bias=bias)
