@@ -19,6 +19,9 @@
 #include "common.h"
 
 // waves per workgroup in split (decode) mode: tuning knob (scripts/tune/), 1 = one split per workgroup
+#ifndef PG_ATTN_FA
+#define PG_ATTN_FA 1      // prefill: the LDS-DMA flash kernel (0: the register-staged kernels)
+#endif
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
@@ -373,6 +376,162 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
   }
 }
 
+// Prefill flash attention, LDS-DMA staged (no mask, 16-B aligned strides).  A workgroup of WAVES waves
+// (16 query rows each) walks 64-key blocks; every block's K [64 keys][DP] and V^T [DT*16 d][64 keys] are
+// pulled HBM->LDS by global_load_lds (16 B/lane, lane-linear destinations) into a 2-stage ring, the next
+// block in flight while the current one is computed.  Images:
+//   K   : 16-key groups of [DP/8 chunks][16 keys][16 B] -> a S^T fragment read (16 keys x 32 d) is one
+//         contiguous KiB per wave-instruction (conflict-free ds_read_b128)
+//   V^T : rows of 128 B (64 keys), 16-B chunk XOR-swizzled by (row >> 1) & 7 through the source address
+//         -> the two ds_read_b64 of a PV fragment are conflict-free
+// Per block a wave does 4 x KS S^T MFMAs, an online softmax on 16 scores per lane (the rescale of O is
+// skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
+// V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row).
+template <int DP, int DT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
+  constexpr int KS = DP / 32;
+  constexpr int NCH = DP / 8;                      // 16-B chunks per K row
+  constexpr int KIMG = 64 * DP * 2;                // bytes
+  constexpr int VIMG = DT * 16 * 128;
+  constexpr int STAGE = KIMG + VIMG;
+  constexpr int KINS = KIMG / 1024, VINS = VIMG / 1024;   // glds wave-instructions per block
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int t = threadIdx.x;
+  const int lane = t & 63, wave = t >> 6, c = lane & 15, g = lane >> 4;
+  const int b = blockIdx.z, kvh = blockIdx.y;
+  const int Lkv = a.Lkv;
+  const int R = a.Lq * a.G;
+  const int D = a.D;
+  const int r = (blockIdx.x * WAVES + wave) * 16 + c;
+  const bool rvalid = r < R;
+  const int pos = rvalid ? r / a.G : 0;
+  const int hq = kvh * a.G + (rvalid ? r % a.G : 0);
+
+  bf16x8 qf[KS];
+  {
+    const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int d0 = 32 * s + 8 * g;
+      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
+    }
+  }
+  const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
+  const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
+  const int vkey_max = ((Lkv + 7) & ~7) - 8;       // last readable 8-key chunk of a V^T row
+
+  auto stage = [&](int kb, int buf) {
+    char* kimg = smem + buf * STAGE;
+    char* vimg = kimg + KIMG;
+    for (int i = wave; i < KINS; i += WAVES) {
+      const int kg = i / (NCH / 4), cq = i % (NCH / 4);
+      const int ch = 4 * cq + (lane >> 4), key = 16 * kg + (lane & 15);
+      const bf16_t* src = kbase + (long)min(kb + key, Lkv - 1) * a.k_rs + ch * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(kimg + i * 1024), 16, 0, 0);
+    }
+    for (int i = wave; i < VINS; i += WAVES) {
+      const int row = 8 * i + (lane >> 3);
+      const int cl = (lane & 7) ^ ((row >> 1) & 7);
+      const bf16_t* src = vbase + (long)min(row, D - 1) * a.vt_ds + min(kb + 8 * cl, vkey_max);
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(vimg + i * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) o[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const int nblk = (Lkv + 63) / 64;
+
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int ib = 0; ib < nblk; ++ib) {
+    const int kb = ib * 64;
+    if (ib + 1 < nblk) stage(kb + 64, (ib + 1) & 1);   // that buffer was last read before the previous barrier
+    const char* kimg = smem + (ib & 1) * STAGE;
+    const char* vimg = kimg + KIMG;
+    // ---- S^T for 4 groups of 16 keys
+    f32x4 sc[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const bf16x8 kf = *(const bf16x8*)(kimg + ((kt * NCH + 4 * s + g) * 16 + c) * 16);
+        sc[kt] = mfma16(kf, qf[s], sc[kt]);
+      }
+    // lane holds S[key = kb + 16 kt + 4g + j][q = c]
+    float x[16];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[kt][j] * a.scale_log2;
+    if (kb + 64 > Lkv) {
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (kb + 16 * kt + 4 * g + j >= Lkv) x[4 * kt + j] = -INFINITY;
+    }
+    float bm = x[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) bm = fmaxf(bm, x[j]);
+    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    const float mn = fmaxf(m, bm);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O
+#pragma unroll
+      for (int tt = 0; tt < DT; ++tt) o[tt] *= alpha;
+    }
+    // ---- O^T += V^T . P^T over two 32-key steps; slot 8g+j <-> key 32h + 4g + j (j < 4), 32h + 16 + 4g + j - 4
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      u32x4 pw;
+      pw[0] = pack_bf2(x[8 * h + 0], x[8 * h + 1]);
+      pw[1] = pack_bf2(x[8 * h + 2], x[8 * h + 3]);
+      pw[2] = pack_bf2(x[8 * h + 4], x[8 * h + 5]);
+      pw[3] = pack_bf2(x[8 * h + 6], x[8 * h + 7]);
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+      for (int tt = 0; tt < DT; ++tt) {
+        const int row = 16 * tt + c;
+        const char* vr = vimg + row * 128;
+        const int sw = (row >> 1) & 7;
+        const int c0 = 4 * h, c1 = 4 * h + 2;                 // 16-B chunks of keys 32h + 4g.. and 32h + 16 + 4g..
+        const u32x2 v0 = *(const u32x2*)(vr + ((c0 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
+        const u32x2 v1 = *(const u32x2*)(vr + ((c1 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
+        o[tt] = mfma16(__builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]}), pf, o[tt]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next block landed (this wave's loads)
+    __builtin_amdgcn_s_barrier();                        // ... every wave's; this buffer fully read
+  }
+  if (!rvalid) return;
+  const float inv = 1.0f / l;
+  bf16_t* op = a.o + ((long)b * a.Lq + pos) * a.o_rs + (long)hq * D;
+#pragma unroll
+  for (int tt = 0; tt < DT; ++tt) {
+    const int d = 16 * tt + 4 * g;
+    if (d < D) {
+      u32x2 p;
+      p[0] = pack_bf2(o[tt][0] * inv, o[tt][1] * inv);
+      p[1] = pack_bf2(o[tt][2] * inv, o[tt][3] * inv);
+      *(u32x2*)(op + d) = p;
+    }
+  }
+}
+
 // Merge the split partials: out[b][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s.
 // One workgroup per (b, kv head, q row of the group), one thread per d.
 __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restrict__ part_o,
@@ -416,7 +575,11 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 
 #define ATTN_DISPATCH(DP_, DT_)                                                             \
   if (DP == DP_ && DT == DT_) {                                                              \
-    if (use_lds)                                                                             \
+    if (fa_waves == 8)                                                                       \
+      hipLaunchKernelGGL((attn_fa_kernel<DP_, DT_, 8>), grid, dim3(512), 0, stream, a);      \
+    else if (fa_waves == 4)                                                                  \
+      hipLaunchKernelGGL((attn_fa_kernel<DP_, DT_, 4>), grid, dim3(256), 0, stream, a);      \
+    else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
     else                                                                                     \
       hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(split_keys > 0 ? 64 * PG_ATTN_SPLIT_WAVES : 64), 0, \
@@ -446,9 +609,19 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
   // prefill with >= 1024 one-wave workgroups: the LDS-staged kernel (64 rows per workgroup share K/V);
   // needs 16-B aligned V^T rows / batch offsets
   const long wgs16 = (long)((Lq * G + 15) / 16) * Hkv * B;
-  const bool use_lds = split_keys == 0 && wgs16 >= 1024 && vt_ds % 8 == 0 && vt_bs % 8 == 0 && vt_hs % 8 == 0 &&
-                       k_rs % 8 == 0 && k_bs % 8 == 0 && k_hs % 8 == 0 && q_rs % 8 == 0;
-  if (use_lds) {
+  const bool aligned = vt_ds % 8 == 0 && vt_bs % 8 == 0 && vt_hs % 8 == 0 && k_rs % 8 == 0 && k_bs % 8 == 0 &&
+                       k_hs % 8 == 0 && q_rs % 8 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 &&
+                       ((uintptr_t)vt & 15) == 0;
+  // LDS-DMA flash kernel for every unmasked prefill; 8 waves (128 rows) per workgroup once that fills the chip
+  int fa_waves = 0;
+  if (split_keys == 0 && mask == nullptr && aligned && lkv_dev == nullptr && PG_ATTN_FA) {
+    const long wg128 = (long)((Lq * G + 127) / 128) * Hkv * B;
+    fa_waves = wg128 >= 256 ? 8 : 4;
+    grid = dim3((Lq * G + 16 * fa_waves - 1) / (16 * fa_waves), Hkv, B);
+  }
+  const bool use_lds = fa_waves == 0 && split_keys == 0 && wgs16 >= 1024 && aligned;
+  if (fa_waves) {
+  } else if (use_lds) {
     grid = dim3((Lq * G + 63) / 64, Hkv, B);
   } else if (split_keys > 0) {
     PG_REQUIRE(Lq * G <= 16 && nsplit % 4 == 0 && part_o && part_ml && split_keys % 32 == 0);
