@@ -20,6 +20,10 @@
 // modeling_paligemma.py:57, modeling_gemma.py:205-207,255-259,484.
 #include "common.h"
 
+#ifndef PG_G256_PREFETCH
+#define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
+#endif
+
 enum {
   PG_EPI_BF16 = 0,          // C bf16 = acc + bias
   PG_EPI_BF16_GELU = 1,     // C bf16 = gelu_tanh(acc + bias)
@@ -417,21 +421,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[4][2], fb[2][2];
+  // fragment registers: A rows [0,64) / [64,128) of the wave (fa0 / fa1), B columns [0,32) / [32,64) (fb0 / fb1)
+  bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
 
-  auto read_a = [&](const char* img) {
+  auto read_a = [&](const char* img, bf16x8 (&fa)[4][2]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(img, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
   };
-  auto read_b = [&](const char* img) {
+  auto read_b = [&](const char* img, bf16x8 (&fb)[2][2]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int s = 0; s < 2; ++s) fb[j][s] = lds_frag(img, wc * 32 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
   };
-  auto mma = [&](int rh, int ch) {
+  auto mma = [&](int rh, int ch, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -457,26 +462,47 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * 4 * HALF;
-    // phase 0: quadrant (rows 0-63, cols 0-31) from A0, B0; restage B0 of tile t+1
-    read_a(buf);
-    read_b(buf + 2 * HALF);
+#if PG_G256_PREFETCH
+    // the reads of phases 1-3 are issued one phase early, ahead of the current phase's MFMAs (tile t is
+    // retired for every wave from phase 0 on; each half is still restaged only after its last read)
+    read_a(buf, fa0);
+    read_b(buf + 2 * HALF, fb0);
     if (t + 1 < nk) stage(2, t + 1);
-    mma(0, 0);
+    read_b(buf + 3 * HALF, fb1);
+    mma(0, 0, fa0, fb0);
+    __builtin_amdgcn_s_barrier();
+    read_a(buf + 1 * HALF, fa1);
+    if (t + 2 < nk) stage(0, t + 2);
+    mma(0, 1, fa0, fb1);
+    __builtin_amdgcn_s_barrier();
+    read_b(buf + 2 * HALF, fb0);
+    if (t + 2 < nk) stage(3, t + 2);
+    mma(1, 1, fa1, fb1);
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) stage(1, t + 2);
+    mma(1, 0, fa1, fb0);
+#else
+    // phase 0: quadrant (rows 0-63, cols 0-31) from A0, B0; restage B0 of tile t+1
+    read_a(buf, fa0);
+    read_b(buf + 2 * HALF, fb0);
+    if (t + 1 < nk) stage(2, t + 1);
+    mma(0, 0, fa0, fb0);
     __builtin_amdgcn_s_barrier();
     // phase 1: (rows 0-63, cols 32-63) A regs kept, B1; restage A0 of tile t+2 (A0 was last read in phase 0)
-    read_b(buf + 3 * HALF);
+    read_b(buf + 3 * HALF, fb0);
     if (t + 2 < nk) stage(0, t + 2);
-    mma(0, 1);
+    mma(0, 1, fa0, fb0);
     __builtin_amdgcn_s_barrier();
     // phase 2: (rows 64-127, cols 32-63) A1, B regs kept; restage B1 of tile t+2
-    read_a(buf + 1 * HALF);
+    read_a(buf + 1 * HALF, fa0);
     if (t + 2 < nk) stage(3, t + 2);
-    mma(1, 1);
+    mma(1, 1, fa0, fb0);
     __builtin_amdgcn_s_barrier();
     // phase 3: (rows 64-127, cols 0-31) A regs kept, B0 again; restage A1 of tile t+2; retire tile t+1
-    read_b(buf + 2 * HALF);
+    read_b(buf + 2 * HALF, fb0);
     if (t + 2 < nk) stage(1, t + 2);
-    mma(1, 0);
+    mma(1, 0, fa0, fb0);
+#endif
     if (t + 2 < nk) wait_vm(6); else wait_vm(0);
     __builtin_amdgcn_s_barrier();
   }
