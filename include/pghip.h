@@ -90,6 +90,12 @@ int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, v
             int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
             int aux_ld, int aux_n, hipStream_t stream);
 
+/* Split-K finalisation: C = epilogue(sum_z part[z]) for a GEMM first run with PG_EPI_F32 into nsplit fp32 slabs
+ * [z][M][N] (bias in slab 0).  epi: PG_EPI_BF16 / _GELU / _GELU_MUL / _VT (aux_out, aux_ld, aux_n) / _QKV_ROPE
+ * (fused).  Lets a small-M prefill GEMM with a non-linear epilogue split K across CUs. */
+int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc, int M, int N, int epi, void* aux_out,
+                     int aux_ld, int aux_n, const PgFusedArgs* fused, hipStream_t stream);
+
 /* pg_gemm + fused prologue / RoPE-KV epilogue (decode layer in 5 launches). */
 int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
                   int M, int N, int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream);

@@ -103,11 +103,8 @@ struct EpiArgs {
 // RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
 // the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).
-__device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
-  if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);   // bias in packed (permuted) column order
-  f32x4 pr;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+// v: columns n0..n0+3 (bias added), pr: the same four of the rotate_half partner columns (n0 ^ 8)
+__device__ __forceinline__ void epi_qkv_rope4_pr(const EpiArgs& e, int m, int n0, f32x4 v, f32x4 pr) {
   if (m >= e.M || n0 >= e.N) return;
   const PgFusedArgs& f = e.f;
   const int D = f.head_dim, half = D >> 1;
@@ -144,6 +141,14 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
 #pragma unroll
     for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
   }
+}
+
+__device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
+  if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);   // bias in packed (permuted) column order
+  f32x4 pr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+  epi_qkv_rope4_pr(e, m, n0, v, pr);
 }
 
 // Store 4 consecutive columns n0..n0+3 of row m (values v).  z = split index.
@@ -1029,6 +1034,36 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 }
 
 // --------------------------------------------------------------------------------------
+// Split-K finalisation for the bf16 epilogues (prefill at small M, where a full-K tile grid leaves CUs
+// idle): the GEMM writes fp32 slabs [z][M][N] (bias in slab 0), this kernel sums them and applies the
+// epilogue (bf16 / gelu / gelu*up / V^T side output / RoPE + KV-cache append).  One thread per 4 outputs.
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restrict__ part, int nsplit, EpiArgs e) {
+  const int NO = EPI == PG_EPI_BF16_GELU_MUL ? e.N / 2 : e.N;     // output columns
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const int q4 = NO / 4;
+  if (idx >= (long)e.M * q4) return;
+  const int m = (int)(idx / q4), c0 = (int)(idx % q4) * 4;
+  const size_t slab = (size_t)e.M * e.N;
+  auto sum4 = [&](int n) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < nsplit; ++z) v += *(const f32x4*)(part + z * slab + (size_t)m * e.N + n);
+    return v;
+  };
+  if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+    // output column c0 <- gate column 32*(c0/16) + c0%16, up column +16
+    const int gb = (c0 / 16) * 32, q = c0 % 16;
+    epi_gelu_mul4(e, m, gb, q, sum4(gb + q), sum4(gb + 16 + q));
+  } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+    epi_qkv_rope4_pr(e, m, c0, sum4(c0), sum4(c0 ^ 8));
+  } else {
+    EpiArgs e2 = e;
+    e2.bias = nullptr;                                            // already in slab 0
+    epi_store4<EPI>(e2, m, c0, sum4(c0), 0);
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // C ABI
 // --------------------------------------------------------------------------------------
 // Tile choice: 128-row tiles (2-stage ring, 64 KiB LDS -> 2 workgroups per CU) when that grid already
@@ -1038,7 +1073,7 @@ template <int EPI, bool FRAG>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
-  if (t256 >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
+  if (t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;
     hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
                        (e.M + 255) / 256, (e.N + 255) / 256, e);
@@ -1175,6 +1210,35 @@ extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const flo
                        int aux_ld, int aux_n, hipStream_t stream) {
   return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, aux, aux_rows, aux_out, aux_ld, aux_n,
                    nullptr, stream);
+}
+
+// C = epilogue(sum_z part[z]) for a GEMM run as PG_EPI_F32 with ksplit slabs (bias was applied to slab 0)
+extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc, int M, int N, int epi,
+                                void* aux_out, int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
+  PG_REQUIRE(part != nullptr && nsplit >= 1 && M > 0 && N > 0 && N % 4 == 0);
+  PgFusedArgs f{};
+  if (fa) f = *fa;
+  EpiArgs e{nullptr, C, ldc, M, N, nullptr, 0, (bf16_t*)aux_out, aux_ld, aux_n, f};
+  const int NO = epi == PG_EPI_BF16_GELU_MUL ? N / 2 : N;
+  const long items = (long)M * (NO / 4);
+  const dim3 grid((unsigned)((items + 255) / 256));
+  switch (epi) {
+    case PG_EPI_BF16: hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16>), grid, dim3(256), 0, stream, part, nsplit, e); break;
+    case PG_EPI_BF16_GELU: hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16_GELU>), grid, dim3(256), 0, stream, part, nsplit, e); break;
+    case PG_EPI_BF16_GELU_MUL:
+      PG_REQUIRE(N % 32 == 0);
+      hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16_GELU_MUL>), grid, dim3(256), 0, stream, part, nsplit, e); break;
+    case PG_EPI_BF16_VT:
+      PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
+      hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16_VT>), grid, dim3(256), 0, stream, part, nsplit, e); break;
+    case PG_EPI_QKV_ROPE:
+      PG_REQUIRE(fa && f.head_dim % 16 == 0 && f.cos_t && f.sin_t && f.pos && f.kc && f.vtc && f.rows_per_batch > 0 &&
+                 f.smax > 0 && N == (f.q_heads + 2 * f.kv_heads) * f.head_dim);
+      hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_QKV_ROPE>), grid, dim3(256), 0, stream, part, nsplit, e); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  PG_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,

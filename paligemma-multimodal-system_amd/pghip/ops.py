@@ -70,6 +70,13 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
         _chk(out, torch.bfloat16, "out")
     if M > 16 and K % 64:
         raise ValueError("pghip.gemm: K must be a multiple of 64 for M > 16")
+    s = finalize_split(M, N, K) if ksplit == 1 and epi in _FIN_EPIS else 1
+    if s > 1:   # small-M prefill: split K into fp32 slabs, then the epilogue in pg_gemm_finalize
+        part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)
+        _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(part), N, M, N, K,
+                  (flags & ~0xFF) | EPI_F32, s, None, 0, None, 0, 0, _s())
+        _lib.call("pg_gemm_finalize", _p(part), s, _p(out), ldc, M, N, epi, _p(aux_out), aux_ld, aux_n, None, _s())
+        return out
     _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, flags, ksplit,
               _p(aux), aux_rows, _p(aux_out), aux_ld, aux_n, _s())
     return out
@@ -95,6 +102,15 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
     if ldc is None:
         ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
     lda = A.stride(0) if A is not None else K
+    s = finalize_split(M, N, K) if (fa.pro_mode == 0 and A is not None and ksplit == 1 and
+                                    (epi & 0xFF) in _FIN_EPIS) else 1
+    if s > 1:   # small-M prefill: split K into fp32 slabs, then the (RoPE / KV-append) epilogue
+        part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)
+        _lib.call("pg_gemm", _p(A), lda, _p(W), W.stride(0), _p(bias), _p(part), N, M, N, K,
+                  (epi & ~0xFF) | EPI_F32, s, None, 0, None, 0, 0, _s())
+        _lib.call("pg_gemm_finalize", _p(part), s, _p(out), ldc, M, N, epi & 0xFF, None, 0, 0,
+                  _lib.C.byref(fa), _s())
+        return out
     _lib.call("pg_gemm_fused", _p(A), lda, _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
               _lib.C.byref(fa), _s())
     return out
@@ -206,6 +222,25 @@ def prefetch(t: torch.Tensor, wgs: int = 256, policy: int = 0, nbytes: Optional[
     _lib.call("pg_prefetch", _p(t), n - n % 16, wgs, policy, _s())
 
 
+_FIN_EPIS = (EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_BF16_VT, EPI_QKV_ROPE)
+FINALIZE_SPLIT = True   # tuning switch (scripts/tune): small-M bf16-epilogue GEMMs split K + pg_gemm_finalize
+
+
+def finalize_split(M: int, N: int, K: int) -> int:
+    """K split for a prefill GEMM whose epilogue needs full sums (bf16 / gelu / RoPE ...): used when its
+    full-K tile grid (64x128 tiles, csrc/gemm.hip launch_tile) leaves most CUs idle, as at batch 1; the fp32
+    slabs are then reduced by pg_gemm_finalize.  1 = one launch with the fused epilogue."""
+    if not FINALIZE_SPLIT or M <= 16 or K % 64:
+        return 1
+    if math.ceil(M / 256) * math.ceil(N / 256) >= CUS:
+        return 1
+    tiles = math.ceil(M / 64) * math.ceil(N / 128)
+    if tiles >= 192:
+        return 1
+    s = min(4, math.ceil(CUS / tiles), (K // 64) // 6)
+    return s if s >= 2 else 1
+
+
 def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -> int:
     """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
     s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))
@@ -233,4 +268,9 @@ def gemm_ksplit(M: int, N: int, K: int) -> int:
             if eff > best + 1e-9:
                 best, best_s = eff, s
         return best_s
+    # few 256x256 tiles (prefill at batch 1): a K split deep enough to give every CU one 256-row tile, when
+    # each slice keeps >= 8 k-tiles (W then streams once instead of once per 64-row tile)
+    s256 = math.ceil(CUS / t256)
+    if s256 <= min(16, (K // 64) // 8):
+        return s256
     return split_for(math.ceil(M / 64) * math.ceil(N / 128), K // 64)

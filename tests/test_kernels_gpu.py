@@ -362,12 +362,13 @@ def test_gemm_fused_attention_merge_prologue(B):
     assert err(ref_o, ref) < 2e-2
 
 
-@pytest.mark.parametrize("M,L", [(1, 1), (3, 1), (40, 20), (264, 264)])
-def test_gemm_fused_qkv_rope_epilogue(M, L):
-    """q|k|v GEMM with RoPE + KV append in the epilogue == plain GEMM + pg_rope_kv_write."""
+@pytest.mark.parametrize("M,L,H", [(1, 1, 512), (3, 1, 512), (40, 20, 512), (264, 264, 512), (264, 264, 2048)])
+def test_gemm_fused_qkv_rope_epilogue(M, L, H):
+    """q|k|v GEMM with RoPE + KV append in the epilogue == plain GEMM + pg_rope_kv_write (H = 2048 at M = 264:
+    split K + pg_gemm_finalize)."""
     from pghip import engine, ops
     from pghip.weights import rope_row_perm
-    nh, nkv, hd, H, Smax = 8, 1, 256, 512, 320
+    nh, nkv, hd, Smax = 8, 1, 256, 320
     nblk = nh + 2 * nkv
     W = rnd(nblk * hd, H, scale=1 / 22, seed=25)
     Wp = W.view(nblk, hd, H)[:, rope_row_perm(hd).cuda(), :].reshape(nblk * hd, H).contiguous()
@@ -437,3 +438,31 @@ def test_gemm256_large_m(M, N, K):
         g = (A.float() @ W.float().t()).view(M, N // 32, 2, 16)
         want = (torch.nn.functional.gelu(g[:, :, 0], approximate="tanh") * g[:, :, 1]).reshape(M, N // 2)
         assert err(h, want) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(264, 2560, 2048), (256, 3456, 1152), (256, 640, 1152)])
+def test_split_k_finalize_epilogues(M, N, K):
+    """Small-M bf16-epilogue GEMMs split K into fp32 slabs + pg_gemm_finalize: same outputs as the one-launch
+    fused epilogue (bf16, gelu, gelu*up, V^T side output), up to fp32 summation order."""
+    from pghip import ops
+    assert ops.finalize_split(M, N, K) > 1
+    A, W = rnd(M, K, seed=41), rnd(N, K, scale=1 / math.sqrt(K), seed=42)
+    bias = torch.randn(N).cuda() * 0.1
+    cases = [(ops.EPI_BF16, bias), (ops.EPI_BF16_GELU, bias), (ops.EPI_BF16_GELU_MUL, None)]
+    if N % 12 == 0:                                   # q | k | v with a V^T side output (SigLIP layout)
+        cases.append((ops.EPI_BF16_VT, bias))
+    for epi, bb in cases:
+        outs = []
+        for split in (True, False):
+            ops.FINALIZE_SPLIT = split
+            try:
+                n_out = N // 2 if epi == ops.EPI_BF16_GELU_MUL else N
+                o = torch.zeros(M, n_out, dtype=torch.bfloat16, device="cuda")
+                vt = torch.zeros(N // 3, M, dtype=torch.bfloat16, device="cuda")
+                kw = dict(aux_out=vt, aux_ld=M, aux_n=N - N // 3) if epi == ops.EPI_BF16_VT else {}
+                ops.gemm(A, W, o, epi=epi, bias=bb, **kw)
+                outs.append((o, vt))
+            finally:
+                ops.FINALIZE_SPLIT = True
+        assert err(outs[0][0], outs[1][0]) < 1e-2, epi
+        assert err(outs[0][1].float(), outs[1][1].float()) < 1e-2 or epi != ops.EPI_BF16_VT, epi
