@@ -43,6 +43,7 @@ enum {
 typedef struct PgFusedArgs {
   int pro_mode;             /* 0: x = A ; 1: x = RMSNorm(resid_in + sum partials)*(1+norm_w) (gemma.py:172-181) ;
                                2: x = merge of split-KV attention partials (pg_attn_combine folded in) ;
+                               5: as 2, the attention itself computed in the same launch (pg_attn_oproj only) ;
                                3: x = resid_in*(1+norm_w), rstd from ss_in applied to the outputs (RMSNorm of a
                                   residual finalised by a PG_EPI_F32_FIN producer) ;
                                4: x = A (the producer's fin_x = bf16(resid*(1+norm_w))), rstd from ss_in applied
@@ -89,6 +90,17 @@ typedef struct PgFusedArgs {
 int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
             int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
             int aux_ld, int aux_n, hipStream_t stream);
+
+/* Decode attention + o_proj in one launch (batch <= 2): the split-KV attention of pg_attention's decode mode
+ * (gemma.py:307-339, keys in split_keys blocks, fused->asplit <= 16 splits) is computed by the first
+ * ceil(B*Hkv*asplit/4) workgroups of the o_proj GEMV (gemma.py:356) while the others stream their weights;
+ * every workgroup then merges the partials of its K range and multiplies (fused->pro_mode must be 5; the other
+ * fused fields as for pro_mode 2, plus the PG_EPI_F32_FIN fields).  sync: int[3], zero before the first call,
+ * self-resetting; sync[2] becomes 1 if a wait gave up (bounded spin). */
+int pg_attn_oproj(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const void* vt,
+                  long vt_bs, long vt_hs, long vt_ds, int B, const int* lkv_dev, int Hq, int Hkv, int D, float scale,
+                  int split_keys, int* sync, const void* W, int ldw, void* C, int ldc, int N, int K, int epi,
+                  int ksplit, const PgFusedArgs* fused, hipStream_t stream);
 
 /* Split-K finalisation: C = epilogue(sum_z part[z]) for a GEMM first run with PG_EPI_F32 into nsplit fp32 slabs
  * [z][M][N] (bias in slab 0).  epi: PG_EPI_BF16 / _GELU / _GELU_MUL / _VT (aux_out, aux_ld, aux_n) / _QKV_ROPE

@@ -16,7 +16,7 @@
 // Modes: normal (prefill): a wave walks all keys and writes normalised bf16 O;
 // split (decode): each wave owns a key range and writes (O, m, l) partials that
 // pg_attn_combine merges.
-#include "common.h"
+#include "attn_common.h"
 
 // waves per workgroup in split (decode) mode: tuning knob (scripts/tune/), 1 = one split per workgroup
 #ifndef PG_ATTN_FA
@@ -25,37 +25,6 @@
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
-
-struct AttnArgs {
-  const bf16_t* q; long q_rs;
-  bf16_t* o; long o_rs;
-  const bf16_t* k; long k_bs, k_hs, k_rs;
-  const bf16_t* vt; long vt_bs, vt_hs, vt_ds;
-  const float* mask; long mask_bs, mask_rs;
-  int Lq, Lkv, G, Hkv, D;
-  const int* lkv_dev;      // if set: Lkv = *lkv_dev + Lkv
-  float scale_log2;        // softmax scale * log2(e)
-  int split_keys;          // split mode if > 0 (keys per wave)
-  float* part_o;           // [B][Hkv][nsplit][16][DT*16]
-  float* part_ml;          // [B][Hkv][nsplit][16][2]
-};
-
-// Branch-free guarded loads: the address is always valid (callers clamp it), the value is
-// zeroed by selects.  Conditional loads compiled to branches and, for partial blocks, to
-// serialised per-element loads + vmcnt(0) waits (profiles/r01: decode attention 16 us -> fixed).
-static __device__ __forceinline__ u32x4 ld16_sel(const bf16_t* p, bool ok) {
-  const u32x4 v = *(const u32x4*)p;
-  return u32x4{ok ? v[0] : 0u, ok ? v[1] : 0u, ok ? v[2] : 0u, ok ? v[3] : 0u};
-}
-
-// 4 consecutive keys of one Vt row (row padded so key+3 stays inside), zero beyond kend / invalid d
-static __device__ __forceinline__ u32x2 ld_vt4(const bf16_t* row, int key, int kend, bool dok) {
-  const u32x2 v = *(const u32x2*)(row + key);
-  const int nv = dok ? kend - key : 0;   // number of valid keys among the 4
-  const uint32_t lo = nv >= 2 ? v[0] : (nv == 1 ? (v[0] & 0xFFFFu) : 0u);
-  const uint32_t hi = nv >= 4 ? v[1] : (nv == 3 ? (v[1] & 0xFFFFu) : 0u);
-  return u32x2{lo, hi};
-}
 
 template <int DP, int DT>
 __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
@@ -74,6 +43,10 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int R = a.Lq * a.G;
   const int D = a.D;
 
+  if (split) {
+    attn_decode_split<DP, DT, false>(a, b, kvh, sg * wpg + wave, nsg * wpg, lane);
+    return;
+  }
   const int r0 = split ? 0 : (blockIdx.x * (int)(blockDim.x >> 6) + wave) * 16;
   int kbeg = 0, kend = Lkv, sp = 0;
   if (split) {

@@ -18,7 +18,7 @@
 //
 // Replaces the nn.Linear call sites of modeling_siglip.py:59-62,177-178,
 // modeling_paligemma.py:57, modeling_gemma.py:205-207,255-259,484.
-#include "common.h"
+#include "attn_common.h"
 
 #ifndef PG_G256_PREFETCH
 #define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
@@ -98,6 +98,13 @@ struct EpiArgs {
   int aux_ld;
   int aux_n;
   PgFusedArgs f;
+  // pro_mode 5 (pg_attn_oproj): the first att_wgs workgroups compute the split-KV decode attention (4 splits
+  // each, write-through partials), then every workgroup waits on sync[0] and merges; sync[1] counts the
+  // workgroups done, the last resets both; sync[2] = 1 if a wait gave up
+  AttnArgs att;
+  int att_total;             // B * Hkv * nsplit splits
+  int att_wgs;
+  int* sync;
 };
 
 // RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are
@@ -562,6 +569,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
 #endif
+#ifndef PG_AO_SPLITS_PER_WG
+#define PG_AO_SPLITS_PER_WG 1   // pg_attn_oproj: attention splits per workgroup (one wave each, <= 4)
+#endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
 #endif
@@ -682,10 +692,36 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
     }
     __syncthreads();
     if (t < M) red[64 + t] = rsqrtf((red[t] + red[16 + t] + red[32 + t] + red[48 + t]) / (float)K + f.eps);
-  } else if constexpr (PRO == 2 && PG_MERGE_V2) {
+  } else if constexpr ((PRO == 2 && PG_MERGE_V2) || PRO == 5) {
+    if constexpr (PRO == 5) {
+      // attention role (workgroups [0, att_wgs)): 4 splits, one per wave; then publish (drained write-through
+      // stores, workgroup barrier, one relaxed agent-scope add).  Every workgroup then waits for all of them.
+      const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+      if (wg < e.att_wgs) {
+        const int id = wg * PG_AO_SPLITS_PER_WG + (t >> 6);
+        if ((t >> 6) < PG_AO_SPLITS_PER_WG && id < e.att_total) {
+          const int ns = f.asplit;
+          const int sp = id % ns, kvh = (id / ns) % e.att.Hkv, b = id / (ns * e.att.Hkv);
+          const int DT = (e.att.D + 15) / 16;
+          if (DT == 16) attn_decode_split<256, 16, true>(e.att, b, kvh, sp, ns, t & 63);
+          else if (DT <= 2) attn_decode_split<32, 2, true>(e.att, b, kvh, sp, ns, t & 63);
+          else if (DT <= 4) attn_decode_split<64, 4, true>(e.att, b, kvh, sp, ns, t & 63);
+          else attn_decode_split<128, 8, true>(e.att, b, kvh, sp, ns, t & 63);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) __hip_atomic_fetch_add(e.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (t == 0) {
+        int n = 0;
+        while (__hip_atomic_load(e.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.att_wgs && ++n < (1 << 20))
+          __builtin_amdgcn_s_sleep(2);
+        if (n >= (1 << 20)) __hip_atomic_store(e.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+    }
     // one pass per (row, head, 4 dims): online merge over the splits, no LDS staging / barriers
     const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
-    const int Seff = (f.slot_dev && f.akeys > 0) ? min(S, (*f.slot_dev + f.akeys) / f.akeys) : S;
     const int h0 = k0 / D, nh = Kr / D, D4 = D >> 2;
     const int items = PG_T_NOMERGE ? 0 : M * nh * D4;   // PG_T_NOMERGE: timing experiment only (x = 0)
     if (PG_T_NOMERGE)
@@ -702,10 +738,10 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
 #pragma unroll
         for (int sp = 0; sp < 16; ++sp) {
           const long bs = base0 + (long)min(sp, S - 1) * 16;
-          const f32x2 v = *(const f32x2*)(f.part_ml + bs * 2);
+          const f32x2 v = PRO == 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
           ms[sp] = sp < S ? v[0] : -INFINITY;
           ls[sp] = v[1];
-          o4[sp] = *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+          o4[sp] = PRO == 5 ? ld16_wt(f.part_o + bs * f.dtw + d4 * 4) : *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
         }
         float mx = ms[0];
 #pragma unroll
@@ -725,8 +761,16 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
       }
       __syncthreads();
+      if (PRO == 5 && t == 0) {
+        const int total = gridDim.x * gridDim.y;
+        if (__hip_atomic_fetch_add(e.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+          __hip_atomic_store(e.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);       // every wait is over
+          __hip_atomic_store(e.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       return;
     }
+    const int Seff = (f.slot_dev && f.akeys > 0) ? min(S, (*f.slot_dev + f.akeys) / f.akeys) : S;
     for (int idx = t; idx < items; idx += 256) {
       const int m = idx / (nh * D4), rem = idx % (nh * D4), hl = rem / D4, d4 = rem % D4;
       const int hq = h0 + hl;
@@ -896,7 +940,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     }
   };
   constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
-  if constexpr (STAGED && PG_GEMV_PREW) {
+  // weights issued before the prologue, except by the attention workgroups of pro_mode 5 (their publish
+  // drains vmcnt: the attention result, not their weights, is on everyone's critical path)
+  const bool prew = STAGED && PG_GEMV_PREW && !(PRO == 5 && (int)(blockIdx.y * gridDim.x + blockIdx.x) < e.att_wgs);
+  if (prew) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
       if (d < mine) loadw(d, wb[d]);
@@ -908,7 +955,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
     if (d < mine) {
-      if (!(STAGED && PG_GEMV_PREW)) loadw(d, wb[d]);
+      if (!prew) loadw(d, wb[d]);
       loadx(d, xb[d]);
     }
   for (int base = 0; base < mine; base += DEPTH) {
@@ -1108,7 +1155,7 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
     lds = (lds + 15) & ~(size_t)15;
     if (PRO == 1) lds += 64 * sizeof(float);
     if (PRO == 3) lds += 80 * sizeof(float);
-    if (PRO == 2) {
+    if (PRO == 2 || PRO == 5) {
       const int pairs = e.M * (per_z * CH / e.f.head_dim);
       lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
     }
@@ -1131,6 +1178,9 @@ static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
     case 2: launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 3: launch_gemv_pro<EPI, 3, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 4: launch_gemv_pro<EPI, 4, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 5:
+      if constexpr (EPI == PG_EPI_F32_FIN || EPI == PG_EPI_F32) launch_gemv_pro<EPI, 5, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+      break;
     default: launch_gemv_pro<EPI, 0, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
   }
 }
@@ -1147,7 +1197,8 @@ static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K
 
 static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
                      int M, int N, int K, int epi_flags, int ksplit, const float* aux, int aux_rows, void* aux_out,
-                     int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
+                     int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream,
+                     const AttnArgs* att = nullptr, int att_total = 0, int* sync = nullptr) {
   const bool frag = (epi_flags & PG_W_FRAG) != 0;
   const int epi = epi_flags & 0xFF;
   PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG)) == 0);
@@ -1159,13 +1210,25 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
+  if (f.pro_mode == 5) {
+    PG_REQUIRE(att != nullptr && sync != nullptr && att_total > 0 && f.asplit <= 16 && M <= 2 &&
+               (epi == PG_EPI_F32_FIN || epi == PG_EPI_F32) && att->D <= 256);
+    e.att = *att;
+    e.att_total = att_total;
+    e.att_wgs = (att_total + PG_AO_SPLITS_PER_WG - 1) / PG_AO_SPLITS_PER_WG;
+    e.sync = sync;
+    PG_REQUIRE(e.att_wgs <= ((N + 15) / 16) * ksplit);            // attention roles are a prefix of the grid
+  } else {
+    PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 4);
+  }
   if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
   if (f.pro_mode == 4) PG_REQUIRE(M <= 2 && ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_n <= 256 &&
                                   (M == 1 || f.ss_n <= 128) && f.ss_ld >= f.ss_n);
   if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
   if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
-  if (f.pro_mode == 2) PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 &&
-                                  f.asplit > 0 && f.q_per_kv > 0 && f.kv_heads > 0);
+  if (f.pro_mode == 2 || f.pro_mode == 5)
+    PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 && f.asplit > 0 &&
+               f.q_per_kv > 0 && f.kv_heads > 0);
   if (epi == PG_EPI_QKV_ROPE) PG_REQUIRE(f.head_dim % 16 == 0 && f.cos_t && f.sin_t && f.pos && f.kc && f.vtc &&
                                          f.rows_per_batch > 0 && f.smax > 0 && ksplit == 1 &&
                                          N == (f.q_heads + 2 * f.kv_heads) * f.head_dim);
@@ -1210,6 +1273,23 @@ extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const flo
                        int aux_ld, int aux_n, hipStream_t stream) {
   return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, aux, aux_rows, aux_out, aux_ld, aux_n,
                    nullptr, stream);
+}
+
+// Decode attention + o_proj in one launch (pro_mode 5): the split-KV attention of pg_attention (decode mode)
+// runs in the first workgroups of the o_proj GEMV, the others stream their weights meanwhile, then every
+// workgroup merges the partials of its K range (the pg_gemm_fused pro_mode 2 prologue) and multiplies.
+extern "C" int pg_attn_oproj(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const void* vt,
+                             long vt_bs, long vt_hs, long vt_ds, int B, const int* lkv_dev, int Hq, int Hkv, int D,
+                             float scale, int split_keys, int* sync, const void* W, int ldw, void* C, int ldc, int N,
+                             int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream) {
+  PG_REQUIRE(fused != nullptr && fused->pro_mode == 5 && B > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && D % 8 == 0 &&
+             split_keys % 32 == 0 && split_keys > 0 && fused->head_dim == D && fused->kv_heads == Hkv &&
+             fused->q_per_kv == Hq / Hkv && fused->part_o && fused->part_ml);
+  AttnArgs a{(const bf16_t*)q, q_rs, nullptr, 0, (const bf16_t*)k, k_bs, k_hs, k_rs, (const bf16_t*)vt, vt_bs, vt_hs,
+             vt_ds, nullptr, 0, 0, 1, 1, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys,
+             (float*)fused->part_o, (float*)fused->part_ml};
+  return gemm_impl(nullptr, K, W, ldw, nullptr, C, ldc, B, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream,
+                   &a, B * Hkv * fused->asplit, sync);
 }
 
 // C = epilogue(sum_z part[z]) for a GEMM run as PG_EPI_F32 with ksplit slabs (bias was applied to slab 0)

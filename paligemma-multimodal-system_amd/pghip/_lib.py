@@ -33,6 +33,8 @@ SIGNATURES = {
     "pg_abi_version": [],
     "pg_gemm": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp],
     "pg_gemm_fused": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, C.POINTER(PgFusedArgs), vp],
+    "pg_attn_oproj": [vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, i32, vp, i32, i32, i32, f32, i32, vp, vp, i32,
+                      vp, i32, i32, i32, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,

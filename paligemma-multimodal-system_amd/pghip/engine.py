@@ -67,6 +67,8 @@ class PaliGemmaEngine:
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
+    FUSE_ATTN_O = False     # with USE_FIN: the split-KV attention inside the o_proj launch (pg_attn_oproj): correct,
+                            # measured 1.31 vs 1.19 ms/token (the fused GEMV drops to 1 wave/SIMD; 252 pollers)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -372,14 +374,24 @@ class PaliGemmaEngine:
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=tiles, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
-            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
-                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
-            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
-                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK,
-                                fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
-            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
+            fused = self.FUSE_ATTN_O and nsplit <= 16
+            if not fused:
+                ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                              cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                              B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                              scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
+                              part_ml=part_ml)
+            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_INLINE if fused else ops.PRO_ATTN_COMBINE, part_o=part_o,
+                                part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv,
+                                slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles,
+                                fin_x=xq, norm_w=Lw["post_w"])
+            if fused:   # attention computed by the first workgroups of the o_proj GEMV (one launch)
+                ops.attn_oproj(qb, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd, cache.vt[i], kvd * cache.Smax,
+                               hd * cache.Smax, cache.Smax, Lw["o_w"], part, fa, self._zeros("d_attn_sync", (4,),
+                               torch.int32), B=B, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                               scale=1.0 / math.sqrt(hd), split_keys=SK, epi=ops.EPI_F32_FIN | w.wflag, ksplit=so)
+            else:
+                ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
             fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
             ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)

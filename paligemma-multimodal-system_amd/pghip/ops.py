@@ -14,7 +14,7 @@ import torch
 from . import _lib
 
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN = range(8)
-PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
+PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD, PRO_ATTN_INLINE = range(6)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
 
@@ -112,6 +112,21 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
                   _lib.C.byref(fa), _s())
         return out
     _lib.call("pg_gemm_fused", _p(A), lda, _p(W), W.stride(0), _p(bias), _p(out), ldc, M, N, K, epi, ksplit,
+              _lib.C.byref(fa), _s())
+    return out
+
+
+def attn_oproj(q, q_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, W, out, fa, sync, *, B, lkv_dev, Hq, Hkv, D,
+               scale, split_keys, epi, ksplit, N=None, ldc=None):
+    """pg_attn_oproj: split-KV decode attention computed inside the o_proj GEMV launch (fa.pro_mode = 5)."""
+    _chk(W, torch.bfloat16, "W")
+    _chk_frag(W, epi)
+    _chk(sync, torch.int32, "sync")
+    N = W.shape[0] if N is None else N
+    K = W.shape[1]
+    ldc = N if ldc is None else ldc
+    _lib.call("pg_attn_oproj", _p(q), q_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds, B, _p(lkv_dev),
+              Hq, Hkv, D, float(scale), split_keys, _p(sync), _p(W), W.stride(0), _p(out), ldc, N, K, epi, ksplit,
               _lib.C.byref(fa), _s())
     return out
 

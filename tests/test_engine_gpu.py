@@ -63,14 +63,16 @@ def test_tiny_greedy_matches_reference_loop(tiny, golden):
         assert out[0].tolist() == g["greedy_ids"].tolist()
 
 
-@pytest.mark.parametrize("fuse_max_b,use_fin", [(2, True), (2, False), (0, True)])
-def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin):
+@pytest.mark.parametrize("fuse_max_b,use_fin,attn_o", [(2, True, True), (2, True, False), (2, False, False),
+                                                        (0, True, False)])
+def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin, attn_o):
     """Long decode (no EOS stop) with the oracle's greedy continuation: per-step logits.  Layer forms:
-    in-kernel split-K finalisation (default, single rank), split-K partials reduced by the next GEMV's
-    RMSNorm prologue (the TP form), and the unfused layer (fuse_max_b=0, the B > 2 path)."""
+    in-kernel split-K finalisation with the attention inside the o_proj launch (default, single rank) or as
+    its own kernel, split-K partials reduced by the next GEMV's RMSNorm prologue (the TP form), and the
+    unfused layer (fuse_max_b=0, the B > 2 path)."""
     from oracle import paligemma_oracle as O
     eng, orc = tiny
-    eng.FUSE_MAX_B, eng.USE_FIN = fuse_max_b, use_fin
+    eng.FUSE_MAX_B, eng.USE_FIN, eng.FUSE_ATTN_O = fuse_max_b, use_fin, attn_o
     g = golden("tiny")
     ids_np = g["b1_input_ids"]
     steps = 24
@@ -88,7 +90,30 @@ def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin)
         top = np.sort(ref_logits[t][0])[::-1]
         if top[0] - top[1] > 0.1:
             assert int(st["ids"][0]) == ref_ids[t], t
-    eng.FUSE_MAX_B, eng.USE_FIN = type(eng).FUSE_MAX_B, type(eng).USE_FIN
+    eng.FUSE_MAX_B, eng.USE_FIN, eng.FUSE_ATTN_O = type(eng).FUSE_MAX_B, type(eng).USE_FIN, type(eng).FUSE_ATTN_O
+    if attn_o:
+        assert int(eng._ws["d_attn_sync"][2]) == 0 and int(eng._ws["d_attn_sync"][0]) == 0   # no give-up, reset
+
+
+def test_attn_oproj_matches_separate_launches(tiny, golden):
+    """pg_attn_oproj (attention inside the o_proj launch) == attention kernel + merge-prologue o_proj:
+    identical greedy tokens and logits over 10 steps (same partials, same merge order)."""
+    eng, _ = tiny
+    g = golden("tiny")
+    ids = torch.from_numpy(g["b1_input_ids"]).cuda()
+    px = torch.from_numpy(g["b1_pixel_values"]).cuda()
+    outs = []
+    for fused in (True, False):
+        eng.FUSE_ATTN_O = fused
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 12)
+        st = eng.decode_state(1, cache, nxt, 12)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(10)]
+        outs.append((st["hist"][:11, 0].tolist(), torch.stack(lg)))
+    eng.FUSE_ATTN_O = type(eng).FUSE_ATTN_O
+    assert outs[0][0] == outs[1][0]
+    assert err(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy()) < 1e-5
+    assert int(eng._ws["d_attn_sync"][2]) == 0
 
 
 @pytest.mark.slow
