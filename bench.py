@@ -140,6 +140,9 @@ def main():
     ap.add_argument("--batch", type=int, default=1)
     ap.add_argument("--gen-tokens", type=int, default=128)
     ap.add_argument("--parallel", default="dp", choices=["dp", "tp"])
+    ap.add_argument("--comm", default="xgmi", choices=["xgmi", "rccl"],
+                    help="TP all-reduce: pg_allreduce_xgmi for decode-size slabs (RCCL/gloo beyond its buffer), "
+                    "or the process group's collective only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
                     "instead of greedy, as BASELINE configs[3]")
@@ -168,9 +171,10 @@ def main():
     sd = synthetic.SyntheticStateDict(cfg)
     tp = world if args.parallel == "tp" else 1
     if tp > 1:
-        from pghip.tp import TPComm
+        from pghip.tp import TPComm, XgmiComm
+        comm = XgmiComm() if args.comm == "xgmi" else TPComm()
         eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=tp),
-                                     comm=TPComm())
+                                     comm=comm)
     else:
         eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
     torch.cuda.synchronize()
@@ -294,7 +298,7 @@ def main():
 
     baseline_ref = {("pt-224", 1): "BASELINE.json configs[1]", ("pt-448", 16): "BASELINE.json configs[2]"}.get(
         (args.config, B), "not a BASELINE.json config")
-    if tp == 2 and args.sample and args.config == "pt-224":
+    if tp == 2 and args.sample and args.config in ("pt-224", "mix-224"):
         baseline_ref = "BASELINE.json configs[3] (mix-224 = the pt-224 architecture)"
     if rank == 0:
         rec = {
@@ -306,7 +310,7 @@ def main():
             "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
                                    f"{T} {'top-p' if args.sample else 'greedy'} tokens ({baseline_ref})",
                        "global_batch": B * (world // tp), "seq_len": L + T,
-                       "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}", "decode": graph_mode},
+                       "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}-{args.comm}", "decode": graph_mode},
             "prefill_ms": round(prefill_ms, 3),
             "prefill_tflops": round(pf_flops / (prefill_ms / 1e3) / 1e12, 2),
             "prefill_mfma_frac": round(pf_flops / (prefill_ms / 1e3) / 1e12 / BF16_PEAK_TFS, 4),
@@ -322,6 +326,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)
+    if hasattr(eng.comm, "check"):
+        eng.comm.check()                       # a timed-out exchange invalidates the run
     if dist is not None:
         dist.destroy_process_group()
 

@@ -181,6 +181,27 @@ int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, 
  * streams them; no reference counterpart: a scheduling aid of the decode graph).  policy 1 = nt loads. */
 int pg_prefetch(const void* p, long bytes, int wgs, int policy, hipStream_t stream);
 
+/* ---- one-shot all-reduce over xGMI (the reference is single-device, so this
+ * replaces nothing there -- it is the tensor-parallel exchange of the Gemma decoder's o_proj / down_proj
+ * partial sums -- o_proj at modeling_gemma.py:356 and down_proj at modeling_gemma.py:218, split across ranks).
+ * Setup: each rank allocates one exchange buffer of pg_xgmi_buffer_bytes(world, cap) bytes with
+ * pg_xgmi_alloc (uncached device memory), exports it with pg_xgmi_ipc_handle (64-byte handle), and maps
+ * every peer's handle with pg_xgmi_ipc_open.  peers[r] = rank r's buffer as mapped in this process. */
+int pg_xgmi_buffer_bytes(int world, long cap, long* bytes);
+int pg_xgmi_alloc(long bytes, void** out);
+int pg_xgmi_free(void* p);
+int pg_xgmi_ipc_handle(void* p, void* handle64);
+int pg_xgmi_ipc_open(const void* handle64, void** out);
+int pg_xgmi_ipc_close(void* p);
+/* In-place SUM of data[0, n) fp32 over `world` ranks (<= 8): every rank stores its data into slot `rank`
+ * of every peer's buffer, raises a per-workgroup flag there, waits for the peers' flags in its own buffer
+ * and sums the slots in rank order 0..world-1 (bit-identical result on every rank).  epochs: 64 local
+ * zero-initialised u32 words owned by the communicator; err: a local int set to 1 if a peer did not
+ * arrive within 20 s.  n % 4 == 0, n <= cap, data 16-byte aligned.  Device-side state only, so the call
+ * can be captured into a hipGraph; every rank must issue the same sequence of calls. */
+int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
+                      unsigned* epochs, int* err, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

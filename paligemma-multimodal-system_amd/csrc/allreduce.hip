@@ -1,0 +1,164 @@
+// pg_allreduce_xgmi: one-shot SUM all-reduce of fp32 partials between the tensor-parallel ranks of one
+// node, over xGMI peer-to-peer stores (the reference has no parallelism at all).
+//
+// Why not only RCCL: a decode step all-reduces two [B][hidden] fp32 slabs per layer (8-256 KB).  At
+// that size a ring collective is latency-bound (2(W-1) dependent hops); a one-shot exchange is one
+// hop: every rank stores its slab straight into slot `rank` of every peer's exchange buffer (the W-1
+// stores go out over W-1 different xGMI links at once), raises a flag there, waits for the W flags
+// in its own buffer and sums the W slots in rank order 0..W-1 -- so every rank computes the
+// bit-identical sum (the vocabulary-parallel greedy merge depends on ranks agreeing).
+//
+// Exchange buffer of one rank (uncached device memory, mapped into the peers with IPC handles):
+//   [0, 4096)   flags   u32 [2 sets][PG_XG_MAXWG workgroups][PG_XG_MAXW ranks]
+//   [4096, ..)  slots   f32 [2 sets][W][cap]
+// Call e (per workgroup, counted in a local `epochs[wg]` word) uses set e&1 and raises its flags to
+// e.  A rank can only start call e+2 after every peer raised its flags for e+1, i.e. after every
+// peer finished reading set e&1 for call e, so two sets make the reuse race-free.  Everything the
+// kernel needs lives on the device (epoch counters included), so the call is capturable into the
+// decode hipGraph.
+//
+// Waiting is bounded by the 100 MHz wall clock: a peer that never arrives sets err[0] and the kernel
+// finishes (its output is then meaningless) instead of hanging the device.
+#include <cstring>
+
+#include "common.h"
+
+#define PG_XG_MAXW 8
+#define PG_XG_MAXWG 64
+#define PG_XG_FLAG_BYTES 4096
+#define PG_XG_TIMEOUT_TICKS 2000000000ull   // 20 s of the 100 MHz constant clock
+
+struct XgPeers {
+  void* p[PG_XG_MAXW];
+};
+
+template <int W>
+__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__ data, long chunk, long n, int rank,
+                                                             XgPeers peers, long cap, unsigned* __restrict__ epochs,
+                                                             int* __restrict__ err) {
+  const int wg = blockIdx.x, tid = threadIdx.x;
+  const unsigned e = epochs[wg] + 1u;
+  __syncthreads();
+  if (tid == 0) epochs[wg] = e;
+  const int set = (int)(e & 1u);
+  const long c0 = (long)wg * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+
+  // 1. push this rank's chunk into slot `rank` of every peer (and of itself)
+  for (long i = c0 + 4 * tid; i < c1; i += 1024) {
+    const f32x4 v = *(const f32x4*)(data + i);
+#pragma unroll
+    for (int p = 0; p < W; ++p) {
+      float* dst = (float*)((char*)peers.p[p] + PG_XG_FLAG_BYTES) + ((long)set * W + rank) * cap + i;
+      __builtin_nontemporal_store(v, (f32x4*)dst);
+    }
+  }
+  __threadfence_system();   // this thread's slot stores are complete and visible system-wide
+  __syncthreads();          // ... for every thread of the workgroup
+  if (tid < W) {
+    unsigned* f = (unsigned*)peers.p[tid] + (set * PG_XG_MAXWG + wg) * PG_XG_MAXW + rank;
+    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+
+  // 2. wait for the W flags of this workgroup's chunk in the local buffer
+  if (tid < W) {
+    unsigned* f = (unsigned*)peers.p[rank] + (set * PG_XG_MAXWG + wg) * PG_XG_MAXW + tid;
+    const unsigned long long t0 = wall_clock64();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != e) {
+      if (wall_clock64() - t0 > PG_XG_TIMEOUT_TICKS) {
+        atomicExch(err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+
+  // 3. sum the W slots in rank order (identical on every rank)
+  const float* slots = (const float*)((const char*)peers.p[rank] + PG_XG_FLAG_BYTES) + (long)set * W * cap;
+  for (long i = c0 + 4 * tid; i < c1; i += 1024) {
+    f32x4 s = __builtin_nontemporal_load((const f32x4*)(slots + i));
+#pragma unroll
+    for (int p = 1; p < W; ++p) s += __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
+    *(f32x4*)(data + i) = s;
+  }
+}
+
+extern "C" int pg_xgmi_buffer_bytes(int world, long cap, long* bytes) {
+  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && cap > 0 && cap % 4 == 0 && bytes != nullptr);
+  *bytes = PG_XG_FLAG_BYTES + 2L * world * cap * (long)sizeof(float);
+  return 0;
+}
+
+// Uncached device memory (flags and slots are read by the owner while peers write them over xGMI).
+extern "C" int pg_xgmi_alloc(long bytes, void** out) {
+  PG_REQUIRE(out != nullptr && bytes > 0);
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(p, 0, (size_t)bytes);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return (int)e;
+  }
+  *out = p;
+  return 0;
+}
+
+extern "C" int pg_xgmi_free(void* p) { return (int)hipFree(p); }
+
+extern "C" int pg_xgmi_ipc_handle(void* p, void* handle64) {
+  PG_REQUIRE(p != nullptr && handle64 != nullptr);
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) return (int)e;
+  std::memcpy(handle64, &h, sizeof(h));
+  return 0;
+}
+
+extern "C" int pg_xgmi_ipc_open(const void* handle64, void** out) {
+  PG_REQUIRE(handle64 != nullptr && out != nullptr);
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle64, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int pg_xgmi_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+// In-place SUM of data[0, n) over `world` ranks.  peers[r] = rank r's exchange buffer as mapped in this
+// process (peers[rank] = the local one), each pg_xgmi_buffer_bytes(world, cap) long; epochs = PG_XG_MAXWG
+// zero-initialised local u32 words owned by this communicator; err = one local int (set to 1 on a timeout).
+// n % 4 == 0, n <= cap, data 16-B aligned.  Every rank must issue the same sequence of calls.
+extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
+                                 unsigned* epochs, int* err, hipStream_t stream) {
+  PG_REQUIRE(data != nullptr && peers != nullptr && epochs != nullptr && err != nullptr);
+  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && rank >= 0 && rank < world);
+  PG_REQUIRE(n > 0 && n % 4 == 0 && n <= cap && cap % 4 == 0 && ((uintptr_t)data & 15) == 0);
+  XgPeers pp = {};
+  for (int r = 0; r < world; ++r) {
+    PG_REQUIRE(peers[r] != nullptr && ((uintptr_t)peers[r] & 15) == 0);
+    pp.p[r] = peers[r];
+  }
+  // 8192 floats (32 KB) per workgroup at least, at most PG_XG_MAXWG workgroups
+  long chunk = (n + PG_XG_MAXWG - 1) / PG_XG_MAXWG;
+  chunk = chunk < 8192 ? 8192 : (chunk + 3) / 4 * 4;
+  const int wgs = (int)((n + chunk - 1) / chunk);
+#define PG_XG_CASE(WW)                                                                                       \
+  case WW:                                                                                                   \
+    hipLaunchKernelGGL((allreduce_xgmi_kernel<WW>), dim3(wgs), dim3(256), 0, stream, data, chunk, n, rank, pp, \
+                       cap, epochs, err);                                                                    \
+    break;
+  switch (world) {
+    PG_XG_CASE(1)
+    PG_XG_CASE(2)
+    PG_XG_CASE(3)
+    PG_XG_CASE(4)
+    PG_XG_CASE(5)
+    PG_XG_CASE(6)
+    PG_XG_CASE(7)
+    PG_XG_CASE(8)
+  }
+#undef PG_XG_CASE
+  PG_LAUNCH_CHECK();
+  return 0;
+}

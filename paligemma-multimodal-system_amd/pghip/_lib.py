@@ -51,6 +51,13 @@ SIGNATURES = {
     "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
     "pg_prefetch": [vp, i64, i32, i32, vp],
+    "pg_xgmi_buffer_bytes": [i32, i64, C.POINTER(C.c_long)],
+    "pg_xgmi_alloc": [i64, C.POINTER(C.c_void_p)],
+    "pg_xgmi_free": [vp],
+    "pg_xgmi_ipc_handle": [vp, C.c_char_p],
+    "pg_xgmi_ipc_open": [C.c_char_p, C.POINTER(C.c_void_p)],
+    "pg_xgmi_ipc_close": [vp],
+    "pg_allreduce_xgmi": [vp, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
 }
 
 _lib = None

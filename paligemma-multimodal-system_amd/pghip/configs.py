@@ -89,7 +89,8 @@ TINY = {
     },
 }
 
-CONFIGS = {"pt-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY}
+# mix-224 (BASELINE configs[3]) is the pt-224 architecture with fine-tuned weights: same shapes, same path
+CONFIGS = {"pt-224": PT_224, "mix-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY}
 
 
 def num_image_tokens(cfg: dict) -> int:

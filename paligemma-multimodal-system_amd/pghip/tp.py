@@ -3,9 +3,10 @@
 One process per GPU.  The only data-path collective is an in-place SUM all-reduce of
 fp32 partial sums — after o_proj, after down_proj, and for the vocabulary-parallel
 lm_head (each rank writes its slot of a zeroed buffer, so the SUM is an all-gather) —
-issued on the current HIP stream through torch.distributed: backend "nccl" is RCCL
-over xGMI on the MI355X node (capturable into the decode hipGraph), "gloo" is the CPU
-transport used by the world-size-2 tests.  The reference has no parallelism at all
+issued on the current HIP stream, either through torch.distributed (TPComm: backend
+"nccl" is RCCL over xGMI on the MI355X node, capturable into the decode hipGraph; "gloo"
+is the CPU transport used by the world-size-2 tests) or as the one-shot peer-store
+kernel pg_allreduce_xgmi (XgmiComm, csrc/allreduce.hip) for decode-size slabs.  The reference has no parallelism at all
 (single device, modeling_gemma.py / inference.py); this replaces nothing there.
 """
 from __future__ import annotations
@@ -27,6 +28,82 @@ class TPComm:
 
     def all_reduce(self, t: torch.Tensor):
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
+
+
+class XgmiComm(TPComm):
+    """TP communicator whose decode-size all-reduces run as pg_allreduce_xgmi (one-shot peer stores over
+    xGMI, csrc/allreduce.hip); the process group only exchanges the IPC handles at construction and
+    carries what does not fit (non-fp32, unaligned, or more than `cap` elements).
+
+    Every rank holds one exchange buffer; the handles travel through all_gather_object, so this also
+    works over gloo (two ranks sharing one device in the tests).  Because the kernel keeps its epoch
+    counters on the device, the exchange is graph-capturable whatever the backend: `capturable` is
+    True when every all-reduce the engine issues fits (`fits(numel)`)."""
+
+    def __init__(self, group=None, cap: int = 1 << 22):
+        super().__init__(group)
+        import ctypes as C
+        from . import _lib
+        if cap % 4:
+            raise ValueError("XgmiComm: cap must be a multiple of 4")
+        if self.world > 8:
+            raise ValueError("XgmiComm: at most 8 ranks (one node)")
+        self._C, self._lib, self.cap = C, _lib, cap
+        nbytes = C.c_long()
+        _lib.call("pg_xgmi_buffer_bytes", self.world, cap, C.byref(nbytes))
+        own = C.c_void_p()
+        _lib.call("pg_xgmi_alloc", nbytes.value, C.byref(own))
+        self._own = own.value
+        h = C.create_string_buffer(64)
+        _lib.call("pg_xgmi_ipc_handle", self._own, h)
+        handles = [None] * self.world
+        self._dist.all_gather_object(handles, h.raw, group=self.group)
+        self._opened = []
+        peers = (C.c_void_p * self.world)()
+        for r, hr in enumerate(handles):
+            if r == self.rank:
+                peers[r] = self._own
+                continue
+            m = C.c_void_p()
+            _lib.call("pg_xgmi_ipc_open", C.create_string_buffer(hr, 64), C.byref(m))
+            peers[r] = m.value
+            self._opened.append(m.value)
+        self._peers = peers
+        self.epochs = torch.zeros(64, dtype=torch.int32, device="cuda")
+        self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self._dist.barrier(group=self.group)          # every rank mapped every buffer before first use
+        self.capturable = True
+
+    def fits(self, numel: int) -> bool:
+        return 0 < numel <= self.cap and numel % 4 == 0
+
+    def all_reduce(self, t: torch.Tensor):
+        if (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and self.fits(t.numel())
+                and t.data_ptr() % 16 == 0):
+            self._lib.call("pg_allreduce_xgmi", t.data_ptr(), t.numel(), self.rank, self.world, self._peers,
+                           self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+        else:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"XgmiComm: all-reduce of {t.numel()} x {t.dtype} does not fit the exchange "
+                                   f"buffer (cap {self.cap} fp32) inside a graph capture")
+            super().all_reduce(t)
+
+    def check(self):
+        """Raise if any exchange timed out waiting for a peer (results since then are invalid)."""
+        if int(self.err.item()):
+            raise RuntimeError("pg_allreduce_xgmi: a peer did not arrive within the timeout")
+
+    def close(self):
+        if self._own is None:
+            return
+        torch.cuda.synchronize()
+        self._dist.barrier(group=self.group)          # no peer still writes into our buffer
+        for m in self._opened:
+            self._lib.call("pg_xgmi_ipc_close", m)
+        self._dist.barrier(group=self.group)
+        self._lib.call("pg_xgmi_free", self._own)
+        self._own, self._opened = None, []
 
 
 class SoloComm:

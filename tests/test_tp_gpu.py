@@ -24,16 +24,37 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_tp2_engine_on_one_device(tmp_path):
-    if not torch.cuda.is_available():
-        pytest.skip("needs the HIP device")
-    env = dict(os.environ, TP_OUT=str(tmp_path))
+def _launch(worker, tmp_path, **env):
+    env = dict(os.environ, TP_OUT=str(tmp_path), **env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "tp_worker.py")]
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", worker)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
+    return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
+
+
+def test_xgmi_allreduce_two_ranks_on_one_device(tmp_path):
+    """pg_allreduce_xgmi between two processes sharing the device through IPC-mapped exchange buffers:
+    bit-exact against the rank-order fp32 sum for ragged sizes (one and many workgroups, both buffer
+    sets), identical on both ranks, inside a captured hipGraph, and without a timeout."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("xgmi_worker.py", tmp_path)
     for o in res:
+        assert o["err"] == 0, o
+        assert o["bad"] == [], o
+        assert o["graph_bad"] == [], o
+    assert res[0]["digest"] == res[1]["digest"]
+
+
+@pytest.mark.parametrize("comm", ["gloo", "xgmi"])
+def test_tp2_engine_on_one_device(tmp_path, comm):
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("tp_worker.py", tmp_path, TP_COMM=comm)
+    for o in res:
+        assert o["xgmi_err"] == 0, o
+        assert o["graph"] == (comm == "xgmi"), o
         assert o["prefill_err_b1"] < 3e-2 and o["prefill_err_b2"] < 3e-2, o
         assert o["greedy"] == o["greedy_ref"], o
         assert o["decode_slice_err"] < 5e-3, o

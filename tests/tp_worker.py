@@ -1,5 +1,5 @@
 """Rank body of tests/test_tp_gpu.py (launched by torch.distributed.run, 2 ranks on one HIP device,
-gloo transport): the tensor-parallel engine against the reference's golden vectors and the
+gloo transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden vectors and the
 single-rank engine.  Writes one JSON verdict per rank to $TP_OUT/rank<r>.json."""
 import json
 import os
@@ -23,14 +23,15 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     from pghip import configs, engine, synthetic, weights
-    from pghip.tp import TPComm
+    from pghip.tp import TPComm, XgmiComm
     cfg = configs.TINY
     sd = synthetic.SyntheticStateDict(cfg)
+    comm = XgmiComm(cap=1 << 20) if os.environ.get("TP_COMM") == "xgmi" else TPComm()
     tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
-                                comm=TPComm())
+                                comm=comm)
     solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", "tiny.npz")))
-    out = {"rank": rank, "world": world}
+    out = {"rank": rank, "world": world, "comm": type(comm).__name__, "graph": comm.capturable}
     for B in (1, 2):
         p = f"b{B}_"
         ids = torch.from_numpy(g[p + "input_ids"]).cuda()
@@ -75,6 +76,9 @@ def main():
     out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
                                         stop_token=None)[0].tolist()
     torch.cuda.synchronize()
+    out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+    if isinstance(comm, XgmiComm):
+        comm.close()
     with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
     dist.barrier()

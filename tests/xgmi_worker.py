@@ -1,0 +1,76 @@
+"""Rank body of tests/test_tp_gpu.py::test_xgmi_allreduce_two_ranks_on_one_device (torch.distributed.run,
+2 ranks on one HIP device; gloo only carries the IPC handles).  Every rank can regenerate every rank's
+seeded input, so each checks pg_allreduce_xgmi bit-exactly against the fp32 sum in rank order."""
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "paligemma-multimodal-system_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def rank_data(n, r, it):
+    return torch.randn(n, generator=torch.Generator().manual_seed(1000 * it + 17 * r + n))
+
+
+def expected(n, world, it):
+    s = rank_data(n, 0, it)
+    for r in range(1, world):
+        s = s + rank_data(n, r, it)
+    return s
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    torch.cuda.set_device(0)
+    from pghip.tp import XgmiComm
+    comm = XgmiComm(cap=1 << 20)
+    bad, dig = [], hashlib.sha256()
+    # ragged sizes: one workgroup, partial last chunk, many workgroups, the cap itself; each twice (both sets)
+    for it, n in enumerate([4, 1000, 8192, 8196, 2048 * 16, 257216, 3 * 8192 * 64 + 4, 1 << 20] * 2):
+        t = rank_data(n, rank, it).cuda()
+        comm.all_reduce(t)
+        got = t.cpu()
+        if not torch.equal(got, expected(n, world, it)):
+            bad.append([n, it, float((got - expected(n, world, it)).abs().max())])
+        dig.update(got.numpy().tobytes())
+    # captured: three exchanges of different sizes in one graph, replayed with fresh inputs
+    sizes = [2048, 2048 * 16, 4 * 8192]
+    static = [torch.zeros(n, device="cuda") for n in sizes]
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for t in static:
+                comm.all_reduce(t)
+    graph_bad = []
+    for rep in range(4):
+        it = 100 + rep
+        for t, n in zip(static, sizes):
+            t.copy_(rank_data(n, rank, it))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        for t, n in zip(static, sizes):
+            if not torch.equal(t.cpu(), expected(n, world, it)):
+                graph_bad.append([n, rep])
+    out = {"rank": rank, "err": int(comm.err.item()), "bad": bad, "graph_bad": graph_bad,
+           "digest": dig.hexdigest()}
+    del g
+    comm.close()
+    with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
