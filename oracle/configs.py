@@ -89,7 +89,7 @@ TINY = {
     },
 }
 
-CONFIGS = {"pt-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY}
+CONFIGS = {"pt-224": PT_224, "mix-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY}  # mix = pt shapes
 
 
 def num_image_tokens(cfg: dict) -> int:
