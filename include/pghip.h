@@ -75,6 +75,8 @@ typedef struct PgFusedArgs {
   void* fin_x;              /* PG_EPI_F32_FIN (optional): bf16 [M][N] x' = resid*(1+norm_w) for a pro_mode 4 consumer */
   int akeys;                /* pro_mode 2: keys per attention split; with slot_dev (kv length before this token)
                                only the non-empty splits are merged                                            */
+  const float* a_scale;     /* PG_FP8: [M] row scales of A (dequantised A = q * a_scale[m])                      */
+  const float* w_scale;     /* PG_FP8: [N] row scales of W, in W's row order                                   */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -83,6 +85,12 @@ typedef struct PgFusedArgs {
  * ((((t * K/64 + c) * 2 + s) * 64 + 16g + r) * 8 + e): each GEMV wave-instruction then reads 1 KiB
  * contiguous, lane-linear.  Requires N % 16 == 0 and K % 64 == 0; ldw must equal K. */
 #define PG_W_FRAG 0x100
+/* PG_FP8 (pg_gemm_fused only, BASELINE configs[4]): A [M][K] and W [N][K] are fp8 e4m3 (OCP, one byte per
+ * element, lda / ldw in bytes) with per-row scales PgFusedArgs.a_scale / w_scale; the fp32 accumulator of
+ * C[m][n] is multiplied by a_scale[m] * w_scale[n] before the epilogue (bias, gelu*mul, RoPE/KV, fp32 slabs).
+ * 16x16x128 block-scaled MFMA with unit block scales (2x the bf16 rate).  M > 16, K % 128 == 0, lda and ldw
+ * multiples of 16, no prologue, epi in {BF16, BF16_GELU_MUL, F32, QKV_ROPE}. */
+#define PG_FP8 0x200
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
  * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0
@@ -180,6 +188,10 @@ int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, 
 /* Read [p, p + bytes) and discard it (weights pulled into the Infinity Cache ahead of the kernel that
  * streams them; no reference counterpart: a scheduling aid of the decode graph).  policy 1 = nt loads. */
 int pg_prefetch(const void* p, long bytes, int wgs, int policy, hipStream_t stream);
+
+/* fp8 row quantisation feeding PG_FP8 GEMMs: q[m][k] = e4m3(x[m][k] / scale[m]), scale[m] = max|x[m][:]| / 448
+ * (1 for an all-zero row).  x bf16 (row stride ldx), q bytes (row stride ldq).  K, ldx, ldq multiples of 8. */
+int pg_quant_fp8(const void* x, int ldx, int M, int K, void* q, int ldq, float* scale, hipStream_t stream);
 
 /* ---- one-shot all-reduce over xGMI (the reference is single-device, so this
  * replaces nothing there -- it is the tensor-parallel exchange of the Gemma decoder's o_proj / down_proj

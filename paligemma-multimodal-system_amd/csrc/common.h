@@ -34,6 +34,27 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+// fp8 e4m3 (OCP) 16x16x128 with unit block scales (E8M0 127 = 2^0): 2x the bf16 MFMA rate.  Each operand is
+// 32 bytes per lane, given as the two 16-byte chunks (a0, a1) that the bf16 form would consume in two k-steps;
+// A and B take the same byte->k assignment, so any consistent k order gives the same dot product.
+__device__ __forceinline__ f32x4 mfma8(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0, const bf16x8& b1,
+                                       const f32x4& c) {
+  const i32x4 x0 = __builtin_bit_cast(i32x4, a0), x1 = __builtin_bit_cast(i32x4, a1);
+  const i32x4 y0 = __builtin_bit_cast(i32x4, b0), y1 = __builtin_bit_cast(i32x4, b1);
+  const i32x8 a = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const i32x8 b = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+__device__ __forceinline__ f32x4 mfma8(const i32x8& a, const i32x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+__device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(i32x4, lo), __builtin_bit_cast(i32x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

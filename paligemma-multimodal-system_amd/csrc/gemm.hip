@@ -18,6 +18,8 @@
 //
 // Replaces the nn.Linear call sites of modeling_siglip.py:59-62,177-178,
 // modeling_paligemma.py:57, modeling_gemma.py:205-207,255-259,484.
+#include <type_traits>
+
 #include "attn_common.h"
 
 #ifndef PG_G256_PREFETCH
@@ -74,6 +76,10 @@ struct PgFusedArgs {
                              // consumer (x' read like A, rstd from ss_in applied to its outputs)
   int akeys;                 // pro_mode 2: keys per attention split; with slot_dev (= kv length before this
                              // token) only the ceil((*slot_dev + 1) / akeys) non-empty splits are merged
+  // PG_FP8: A and W are fp8 e4m3 with per-row scales (dequantised value = q * scale): the accumulator of
+  // C[m][n] is multiplied by a_scale[m] * w_scale[n] before the epilogue
+  const float* a_scale;      // [M]
+  const float* w_scale;      // [N] (in W's row order, e.g. the packed q|k|v or interleaved gate/up rows)
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -86,6 +92,7 @@ __device__ __forceinline__ f32x4 load4_guard(const float* __restrict__ p, int n0
 }
 
 #define PG_W_FRAG 0x100   // weight layout flag OR-ed into epi (include/pghip.h)
+#define PG_FP8 0x200      // A and W fp8 e4m3 with row scales (PgFusedArgs a_scale / w_scale), M > 16
 
 struct EpiArgs {
   const float* bias;
@@ -106,6 +113,12 @@ struct EpiArgs {
   int att_wgs;
   int* sync;
 };
+
+// fp8 dequantisation of one accumulator fragment: C[m][n0..n0+3] *= a_scale[m] * w_scale[n0..n0+3]
+__device__ __forceinline__ void scale_acc(const EpiArgs& e, int m, int n0, f32x4& v) {
+  if (m >= e.M || n0 >= e.N) return;
+  v *= e.f.a_scale[m] * load4_guard(e.f.w_scale, n0, e.N);
+}
 
 // RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
@@ -273,7 +286,7 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
   }
 }
 
-template <int EPI, int BM, int STAGES, bool FRAG>
+template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false>
 __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                         const bf16_t* __restrict__ W, int ldw, int K, int kchunk,
                                                         int tiles_m, int tiles_n, EpiArgs e) {
@@ -333,18 +346,35 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
     const char* tA = smem + (kt % STAGES) * STAGE_BYTES;
     const char* tW = tA + A_BYTES;
+    if constexpr (F8) {
+      // fp8: the 128-byte k-row holds 128 k; one 16x16x128 MFMA takes both chunk sets of the bf16 form
+      bf16x8 fa[NI][2], fw[NJ][2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int chunk = s * 4 + (lane >> 4);
-      bf16x8 fa[NI], fw[NJ];
+      for (int s = 0; s < 2; ++s) {
+        const int chunk = s * 4 + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) fa[i] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
+        for (int i = 0; i < NI; ++i) fa[i][s] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) fw[j] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
+        for (int j = 0; j < NJ; ++j) fw[j][s] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
+      }
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(fw[j], fa[i], acc[i][j]);
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma8(fw[j][0], fw[j][1], fa[i][0], fa[i][1], acc[i][j]);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int chunk = s * 4 + (lane >> 4);
+        bf16x8 fa[NI], fw[NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) fa[i] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) fw[j] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(fw[j], fa[i], acc[i][j]);
+      }
     }
   }
 
@@ -354,6 +384,10 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
   for (int i = 0; i < NI; ++i) {
     const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
     const int nb = n0 + wn * (TBN / WN);
+    if constexpr (F8) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) scale_acc(e, m, nb + j * 16 + q, acc[i][j]);
+    }
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
 #pragma unroll
       for (int j = 0; j < NJ; j += 2) epi_gelu_mul4(e, m, nb + j * 16, q, acc[i][j], acc[i][j + 1]);
@@ -380,7 +414,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 // B0 of t+1 in phase 0), so 3 half-tiles (6 loads per thread) stay in flight across the raw s_barrier that
 // ends every phase; the single counted wait (vmcnt 6) sits in phase 3 and the tile it retires is read
 // from phase 0 of the next tile on (MI355X guide: 256^2 8-phase template, counted vmcnt, T1/T2/T5).
-template <int EPI, bool FRAG>
+template <int EPI, bool FRAG, bool F8 = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, int K,
                                                       int ktiles_per_split, int tiles_m, int tiles_n, EpiArgs e) {
@@ -433,29 +467,54 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // fragment registers: A rows [0,64) / [64,128) of the wave (fa0 / fa1), B columns [0,32) / [32,64) (fb0 / fb1)
-  bf16x8 fa0[4][2], fa1[4][2], fb0[2][2], fb1[2][2];
+  // fragment registers: A rows [0,64) / [64,128) of the wave (fa0 / fa1), B columns [0,32) / [32,64) (fb0 / fb1);
+  // fp8: both 16-byte chunks of a row in one 8-register operand
+  using FA = std::conditional_t<F8, i32x8[4], bf16x8[4][2]>;
+  using FB = std::conditional_t<F8, i32x8[2], bf16x8[2][2]>;
+  FA fa0, fa1;
+  FB fb0, fb1;
 
-  auto read_a = [&](const char* img, bf16x8 (&fa)[4][2]) {
+  auto read_a = [&](const char* img, auto& fa) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
+      const int row = wr * 64 + i * 16 + (lane & 15);
+      if constexpr (F8) {
+        fa[i] = cat8(lds_frag(img, row, lane >> 4), lds_frag(img, row, 4 + (lane >> 4)));
+      } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(img, wr * 64 + i * 16 + (lane & 15), s * 4 + (lane >> 4));
+        for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(img, row, s * 4 + (lane >> 4));
+      }
+    }
   };
-  auto read_b = [&](const char* img, bf16x8 (&fb)[2][2]) {
+  auto read_b = [&](const char* img, auto& fb) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      const int row = wc * 32 + j * 16 + (lane & 15);
+      if constexpr (F8) {
+        fb[j] = cat8(lds_frag(img, row, lane >> 4), lds_frag(img, row, 4 + (lane >> 4)));
+      } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) fb[j][s] = lds_frag(img, wc * 32 + j * 16 + (lane & 15), s * 4 + (lane >> 4));
+        for (int s = 0; s < 2; ++s) fb[j][s] = lds_frag(img, row, s * 4 + (lane >> 4));
+      }
+    }
   };
-  auto mma = [&](int rh, int ch, const bf16x8 (&fa)[4][2], const bf16x8 (&fb)[2][2]) {
+  auto mma = [&](int rh, int ch, const auto& fa, const auto& fb) {
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+    if constexpr (F8) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[rh * 4 + i][ch * 2 + j] = mfma16(fb[j][s], fa[i][s], acc[rh * 4 + i][ch * 2 + j]);
+        for (int j = 0; j < 2; ++j)
+          acc[rh * 4 + i][ch * 2 + j] = mfma8(fb[j], fa[i], acc[rh * 4 + i][ch * 2 + j]);
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[rh * 4 + i][ch * 2 + j] = mfma16(fb[j][s], fa[i][s], acc[rh * 4 + i][ch * 2 + j]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -525,6 +584,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int nb = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16;
+      if constexpr (F8) scale_acc(e, m, nb + q, acc[i][j]);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int nb = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16;
@@ -1116,13 +1180,14 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // Tile choice: 128-row tiles (2-stage ring, 64 KiB LDS -> 2 workgroups per CU) when that grid already
 // has >= 256 workgroups; otherwise 64-row tiles with a 4-stage ring.  Split-K (fp32 partial epilogue
 // only) is chosen by the caller.
-template <int EPI, bool FRAG>
+// F8: A, W fp8 viewed as bf16-sized pairs (K, lda, ldw in 2-byte units: a 64-unit k-tile = 128 fp8 k)
+template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
   if (t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;
-    hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
+    hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG, F8>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
                        (e.M + 255) / 256, (e.N + 255) / 256, e);
     return;
   }
@@ -1131,13 +1196,13 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   const int t128 = ((e.M + 127) / 128) * tiles_n;
   if (t128 >= 256) {
     const int tiles_m = (e.M + 127) / 128;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st,
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG, F8>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st,
                        A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
     return;
   }
   // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
   const int m64 = (e.M + 63) / 64;
-  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
                      W, ldw, K, kchunk, m64, tiles_n, e);
 }
 
@@ -1200,8 +1265,9 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                      int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream,
                      const AttnArgs* att = nullptr, int att_total = 0, int* sync = nullptr) {
   const bool frag = (epi_flags & PG_W_FRAG) != 0;
+  const bool fp8 = (epi_flags & PG_FP8) != 0;
   const int epi = epi_flags & 0xFF;
-  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG)) == 0);
+  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8)) == 0);
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
@@ -1244,6 +1310,22 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   else PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0 && epi != PG_EPI_F32_FIN);
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
+  if (fp8) {
+    // fp8 e4m3 operands, tile GEMMs only; the kernels see byte pairs, so K / lda / ldw are halved
+    PG_REQUIRE(!frag && M > 16 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && lda % 16 == 0 &&
+               ldw % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0);
+    switch (epi) {
+      case PG_EPI_BF16: launch_tile<PG_EPI_BF16, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+      case PG_EPI_BF16_GELU_MUL:
+        launch_tile<PG_EPI_BF16_GELU_MUL, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+      case PG_EPI_F32: launch_tile<PG_EPI_F32, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+      case PG_EPI_QKV_ROPE:
+        launch_tile<PG_EPI_QKV_ROPE, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    PG_LAUNCH_CHECK();
+    return 0;
+  }
 #define PG_CASE(E)                                                                             \
   case E:                                                                                      \
     if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream);                       \

@@ -1,0 +1,62 @@
+// fp8 e4m3 (OCP) row quantisation for the fp8 GEMM path (BASELINE configs[4]; SURVEY.md §8(a) "fp8 MFMA").
+//
+// q[m][k] = e4m3(x[m][k] / s[m]), s[m] = max_k |x[m][k]| / 448 (1 for an all-zero row): one scale per
+// activation row (token) here, one per output channel for the weights (pghip/weights.py, done once at load).
+// The GEMM multiplies its fp32 accumulator by s_a[m] * s_w[n] before the epilogue (csrc/gemm.hip PG_FP8).
+//
+// x / s is a correctly rounded division (the same value torch computes in pghip/weights.py quant_rows_fp8),
+// and the conversion rounds to nearest even, so both quantisers produce identical bytes.
+// One 256-thread workgroup per row; the row is read twice (the second pass hits L2: a row is <= 32 KB).
+// HBM-bound: 2 + 1 bytes per element.
+#include "common.h"
+
+__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, int ldx, int K,
+                                                             uint8_t* __restrict__ q, int ldq,
+                                                             float* __restrict__ scale) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* xr = x + (size_t)m * ldx;
+  float amax = 0.f;
+  for (int k = tid * 8; k < K; k += 2048) {
+    const u32x4 v = *(const u32x4*)(xr + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fmaxf(fabsf(bf_lo(v[j])), fabsf(bf_hi(v[j]))));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if ((tid & 63) == 0) red[tid >> 6] = amax;
+  __syncthreads();
+  amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = amax > 0.f ? amax / 448.f : 1.f;
+  if (tid == 0) scale[m] = s;
+  uint8_t* qr = q + (size_t)m * ldq;
+  for (int k = tid * 8; k < K; k += 2048) {
+    const u32x4 v = *(const u32x4*)(xr + k);
+    u32x2 o;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float a = fminf(fmaxf(bf_lo(v[2 * j]) / s, -448.f), 448.f);
+      const float b = fminf(fmaxf(bf_hi(v[2 * j]) / s, -448.f), 448.f);
+      const float c = fminf(fmaxf(bf_lo(v[2 * j + 1]) / s, -448.f), 448.f);
+      const float d = fminf(fmaxf(bf_hi(v[2 * j + 1]) / s, -448.f), 448.f);
+      int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+      w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+      o[j] = (uint32_t)w;
+    }
+    *(u32x2*)(qr + k) = o;
+  }
+}
+
+// x bf16 [M][K] (row stride ldx) -> q fp8 e4m3 [M][K] (row stride ldq bytes), scale f32 [M].
+// K % 8 == 0, ldx % 8 == 0, ldq % 8 == 0, 16-byte aligned x.
+extern "C" int pg_quant_fp8(const void* x, int ldx, int M, int K, void* q, int ldq, float* scale, hipStream_t stream) {
+  PG_REQUIRE(x != nullptr && q != nullptr && scale != nullptr && M > 0 && K > 0 && K % 8 == 0 && ldx >= K &&
+             ldx % 8 == 0 && ldq >= K && ldq % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)q & 7) == 0);
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3(M), dim3(256), 0, stream, (const bf16_t*)x, ldx, K, (uint8_t*)q,
+                     ldq, scale);
+  PG_LAUNCH_CHECK();
+  return 0;
+}

@@ -25,7 +25,7 @@ class PgFusedArgs(C.Structure):
                 ("slot_base", C.c_int), ("kc", C.c_void_p), ("vtc", C.c_void_p), ("smax", C.c_int),
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
-                ("akeys", C.c_int)]
+                ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -51,6 +51,7 @@ SIGNATURES = {
     "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
     "pg_prefetch": [vp, i64, i32, i32, vp],
+    "pg_quant_fp8": [vp, i32, i32, i32, vp, i32, vp, vp],
     "pg_xgmi_buffer_bytes": [i32, i64, C.POINTER(C.c_long)],
     "pg_xgmi_alloc": [i64, C.POINTER(C.c_void_p)],
     "pg_xgmi_free": [vp],

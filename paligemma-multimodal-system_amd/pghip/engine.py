@@ -74,6 +74,7 @@ class PaliGemmaEngine:
         self.cfg = cfg
         self.w = weights
         self.comm = comm if comm is not None else SoloComm()
+        self.fp8 = bool(getattr(weights, "fp8", False))
         self.tp = getattr(weights, "tp_world", 1)
         if self.comm.world != self.tp:
             raise ValueError(f"weights packed for tp_world={self.tp}, communicator has world {self.comm.world}")
@@ -183,8 +184,8 @@ class PaliGemmaEngine:
         qb = self._buf("t_q", (T, nh * hd), torch.bfloat16)
         attn = self._buf("t_attn", (T, nh * hd), torch.bfloat16)
         h = self._buf("t_h", (T, I), torch.bfloat16)
-        s_o = ops.gemm_ksplit(T, H, nh * hd) if T > 16 else self.DECODE_SPLIT_O
-        s_d = ops.gemm_ksplit(T, H, I) if T > 16 else self.DECODE_SPLIT_DOWN
+        s_o = self._ksplit(T, H, nh * hd) if T > 16 else self.DECODE_SPLIT_O
+        s_d = self._ksplit(T, H, I) if T > 16 else self.DECODE_SPLIT_DOWN
         part = self._buf("t_part", (max(s_o, s_d), T, H), torch.float32)
         pos = positions.to(device=self.device, dtype=torch.int32).reshape(-1).contiguous()
         ns = 0
@@ -196,17 +197,17 @@ class PaliGemmaEngine:
             # q|k|v projection + RoPE + KV-cache append in one GEMM (modeling_gemma.py:274-302)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=0,
                                 kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
-            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=T)
+            self._lin(xn, Lw, "qkv", qb, ops.EPI_QKV_ROPE, T, fa=fa)
             ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
                           mask_rs=(mask.stride(-2) if mask is not None else 0))
-            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=s_o)
+            self._lin(attn, Lw, "o", part, ops.EPI_F32, T, ksplit=s_o)
             self._allreduce(part[:s_o])
             ops.norm_residual(x_resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=s_o, out=xn)
-            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=s_d)
+            self._lin(xn, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
+            self._lin(h, Lw, "down", part, ops.EPI_F32, T, ksplit=s_d)
             self._allreduce(part[:s_d])
             ns = s_d
             if taps is not None:
@@ -219,6 +220,28 @@ class PaliGemmaEngine:
                           row_map=logits_rows, write_resid=False)
         logits = self.lm_head(xf, rows, fresh=True) if want_logits else None
         return logits, hid
+
+    def _fp8_rows(self, M: int) -> bool:
+        return self.fp8 and M > 16
+
+    def _ksplit(self, M: int, N: int, K: int) -> int:
+        """split-K of an fp32-partial GEMM (fp8 operands: the kernels count K in byte pairs)."""
+        return ops.gemm_ksplit(M, N, K // 2 if self._fp8_rows(M) else K)
+
+    def _lin(self, x: torch.Tensor, Lw: dict, name: str, out: torch.Tensor, epi: int, M: int, ksplit: int = 1,
+             fa=None):
+        """One Gemma linear: bf16 (fragment-packed W) or, with fp8 weights and M > 16, the activation rows
+        quantised to e4m3 (pg_quant_fp8) feeding the PG_FP8 GEMM with the per-channel weight scales."""
+        w = self.w
+        if self._fp8_rows(M):
+            K = x.shape[1]
+            x8 = self._buf(f"x8_{K}", (M, K), torch.uint8)
+            xs = self._buf(f"xs_{K}", (M,), torch.float32)
+            ops.quant_fp8(x, x8, xs, M=M)
+            return ops.gemm8(x8, xs, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa)
+        if fa is not None:
+            return ops.gemm_fused(x, Lw[name + "_w"], out, fa, epi=epi | w.wflag, M=M)
+        return ops.gemm(x, Lw[name + "_w"], out, epi=epi | w.wflag, ksplit=ksplit)
 
     def _allreduce(self, t: torch.Tensor):
         if self.tp > 1:
@@ -414,18 +437,18 @@ class PaliGemmaEngine:
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv)
-            ops.gemm_fused(xn, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
+            self._lin(xn, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=self.DECODE_SPLIT_KEYS, nsplit=nsplit, part_o=part_o,
                           part_ml=part_ml)
             ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
-            ops.gemm(attn, Lw["o_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=so)
+            self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
             self._allreduce(part[:so])
             ops.norm_residual(res, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=so, out=xn)
-            ops.gemm(xn, Lw["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
-            ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=sd)
+            self._lin(xn, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
+            self._lin(h, Lw, "down", part, ops.EPI_F32, B, ksplit=sd)
             self._allreduce(part[:sd])
             ns = sd
         return ns

@@ -82,6 +82,53 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
     return out
 
 
+EPI_FP8 = 0x200   # PG_FP8: A and W fp8 e4m3 with row scales (include/pghip.h)
+
+
+def quant_fp8(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional[torch.Tensor] = None,
+              M: Optional[int] = None):
+    """Row quantisation bf16 [M][K] -> (fp8 e4m3 bytes [M][K] as uint8, fp32 scale [M]) (pg_quant_fp8)."""
+    _chk(x, torch.bfloat16, "x")
+    M = x.shape[0] if M is None else M
+    K = x.shape[1]
+    if q is None:
+        q = torch.empty(M, K, dtype=torch.uint8, device=x.device)
+    if scale is None:
+        scale = torch.empty(M, dtype=torch.float32, device=x.device)
+    if q.dtype != torch.uint8 or q.stride(1) != 1 or x.stride(1) != 1 or q.shape[1] < K or scale.numel() < M:
+        raise ValueError("pghip.quant_fp8: bad output buffers")
+    _lib.call("pg_quant_fp8", _p(x), x.stride(0), M, K, _p(q), q.stride(0), _p(scale), _s())
+    return q, scale
+
+
+def gemm8(A8: torch.Tensor, a_scale: torch.Tensor, W8: torch.Tensor, w_scale: torch.Tensor, out: torch.Tensor, *,
+          epi: int = EPI_BF16, M: Optional[int] = None, bias: Optional[torch.Tensor] = None, ksplit: int = 1,
+          fa=None) -> torch.Tensor:
+    """fp8 GEMM: out = epilogue((A8 . W8^T) * a_scale[m] * w_scale[n]) (PG_FP8, pg_gemm_fused).  A8, W8 are
+    uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE."""
+    for t, n in ((A8, "A8"), (W8, "W8")):
+        if t.dtype != torch.uint8 or not t.is_cuda or t.stride(1) != 1:
+            raise ValueError(f"pghip.gemm8: {n} must be a row-major uint8 (e4m3) HIP tensor")
+    _chk(a_scale, torch.float32, "a_scale")
+    _chk(w_scale, torch.float32, "w_scale")
+    M = A8.shape[0] if M is None else M
+    N, K = W8.shape
+    fa = fused_args() if fa is None else fa
+    fa.a_scale, fa.w_scale = a_scale.data_ptr(), w_scale.data_ptr()
+    e = epi & 0xFF
+    ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
+    s = finalize_split(M, N, K // 2) if ksplit == 1 and e in _FIN_EPIS else 1
+    if s > 1:   # small M: fp32 slabs, then the epilogue (scales already applied inside the slabs)
+        part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)
+        _lib.call("pg_gemm_fused", _p(A8), A8.stride(0), _p(W8), W8.stride(0), _p(bias), _p(part), N, M, N, K,
+                  EPI_F32 | EPI_FP8, s, _lib.C.byref(fa), _s())
+        _lib.call("pg_gemm_finalize", _p(part), s, _p(out), ldc, M, N, e, None, 0, 0, _lib.C.byref(fa), _s())
+        return out
+    _lib.call("pg_gemm_fused", _p(A8), A8.stride(0), _p(W8), W8.stride(0), _p(bias), _p(out), ldc, M, N, K,
+              e | EPI_FP8, ksplit, _lib.C.byref(fa), _s())
+    return out
+
+
 def fused_args(**kw) -> "_lib.PgFusedArgs":
     """Build a PgFusedArgs; tensors are passed as their data pointers."""
     fa = _lib.PgFusedArgs()

@@ -62,10 +62,25 @@ def rope_row_perm(D: int) -> torch.Tensor:
     return torch.tensor(idx, dtype=torch.long)
 
 
+def quant_rows_fp8(w: torch.Tensor):
+    """Per-row (output channel) fp8 e4m3 quantisation of a row-major matrix: (uint8 e4m3 bytes, fp32 scales),
+    w ~= q * scale[:, None], scale = max|row| / 448 (1 for a zero row).  Same rule as pg_quant_fp8."""
+    wf = w.float()
+    amax = wf.abs().amax(1)
+    # tensor / tensor: a correctly rounded division, as in pg_quant_fp8 (torch turns "/ 448.0" into a multiply)
+    scale = torch.where(amax > 0, amax / torch.full_like(amax, 448.0), torch.ones_like(amax))
+    q = (wf / scale[:, None]).clamp_(-448.0, 448.0).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8).contiguous(), scale.contiguous()
+
+
 class PackedWeights:
     def __init__(self, cfg: dict, get, device="cuda", parts=("vision", "proj", "text"), tp_rank: int = 0,
-                 tp_world: int = 1):
+                 tp_world: int = 1, fp8: bool = False):
+        """fp8: also hold the Gemma decoder linears as fp8 e4m3 with per-output-channel scales (`<name>8`,
+        `<name>_s8` in each layer dict) for the PG_FP8 GEMMs of prefill and batch > 16 decode (BASELINE
+        configs[4]); the bf16 copies stay for the weight-streaming GEMV path (batch <= 16 decode)."""
         self.cfg = cfg
+        self.fp8 = bool(fp8)
         self.tp_rank, self.tp_world = int(tp_rank), int(tp_world)
         if not 0 <= self.tp_rank < self.tp_world:
             raise ValueError(f"tp_rank {tp_rank} outside tp_world {tp_world}")
@@ -153,7 +168,7 @@ class PackedWeights:
             raise ValueError("head_dim must be a multiple of 16 for the fused RoPE epilogue")
         self.heads = self.heads_total // W                    # q heads held by this rank
         self.inter_real = self.inter_total // W               # intermediate slice held by this rank
-        self.inter = _rup(self.inter_real, 64)                # kernel width: zero-padded to the GEMM K step
+        self.inter = _rup(self.inter_real, 128 if self.fp8 else 64)   # kernel width: zero-padded to the GEMM K step
         self.vocab_local = self.vocab // W
         self.vocab_offset = R * self.vocab_local
         hd, H, I = self.head_dim, self.hidden, self.inter
@@ -198,9 +213,15 @@ class PackedWeights:
             down[:, :Ir] = bf(get(lp + "mlp.down_proj.weight")[:, i_lo:i_hi])
             o_w = bf(get(a + "o_proj.weight")[:, q_lo:q_hi])
             pk = frag_pack if self.frag else (lambda x: x)
-            self.tl.append(dict(
+            layer = dict(
                 in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=pk(qkv_w), o_w=pk(o_w),
-                post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=pk(gu), down_w=pk(down)))
+                post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=pk(gu), down_w=pk(down))
+            if self.fp8:
+                if H % 128 or (self.heads * hd) % 128:
+                    raise ValueError("fp8 weights need hidden and heads*head_dim multiples of 128")
+                for name, m in (("qkv", qkv_w), ("o", o_w), ("gu", gu), ("down", down)):
+                    layer[name + "_w8"], layer[name + "_s8"] = quant_rows_fp8(m)
+            self.tl.append(layer)
             del qkv_w, o_w, gu, down
             del g, u
         self.final_w = f32(get(lm + "model.norm.weight"))
@@ -220,4 +241,10 @@ class PackedWeights:
     def decode_weight_bytes(self) -> int:
         """HBM bytes of weights one decode step streams (Gemma linears + tied lm_head)."""
         n = sum(sum(d[k].numel() * 2 for k in ("qkv_w", "o_w", "gu_w", "down_w")) for d in self.tl)
+        return n + self.lm_w.numel() * 2
+
+    def decode_weight_bytes_fp8(self) -> int:
+        """The same for the fp8 path (batch > 16 decode): e4m3 linears + scales, bf16 lm_head."""
+        n = sum(sum(d[k + "_w8"].numel() + d[k + "_s8"].numel() * 4 for k in ("qkv", "o", "gu", "down"))
+                for d in self.tl)
         return n + self.lm_w.numel() * 2

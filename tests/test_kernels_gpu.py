@@ -466,3 +466,56 @@ def test_split_k_finalize_epilogues(M, N, K):
                 ops.FINALIZE_SPLIT = True
         assert err(outs[0][0], outs[1][0]) < 1e-2, epi
         assert err(outs[0][1].float(), outs[1][1].float()) < 1e-2 or epi != ops.EPI_BF16_VT, epi
+
+
+# ---------------------------------------------------------------- fp8 e4m3 path (BASELINE configs[4])
+def _deq(q, s):
+    return q.view(torch.float8_e4m3fn).float() * s[:, None]
+
+
+@pytest.mark.parametrize("M,K", [(1, 8), (7, 2048), (300, 16384), (64, 1152)])
+def test_quant_fp8_rows_bit_identical_to_host_rule(M, K):
+    """pg_quant_fp8 (row absmax / 448 scale, RNE e4m3) gives the same bytes and scales as the host rule the
+    weights use (weights.quant_rows_fp8), including an all-zero row (scale 1)."""
+    from pghip import ops
+    from pghip.weights import quant_rows_fp8
+    x = rnd(M, K, scale=3.0, seed=51)
+    x[0] = 0
+    if M > 2:
+        x[1, :] *= 1e-3
+    q, s = ops.quant_fp8(x)
+    q_ref, s_ref = quant_rows_fp8(x)
+    assert torch.equal(s, s_ref)
+    assert torch.equal(q, q_ref)
+    assert err(_deq(q, s), x.float()) < 0.07          # e4m3: 3 mantissa bits
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 384, 512), (1024, 2048, 2048), (4096, 4096, 256), (4200, 4096, 640)])
+def test_gemm_fp8_matches_fp32_matmul_of_dequantised_operands(M, N, K):
+    """PG_FP8 GEMM (16x16x128 block-scaled MFMA, unit block scales, row scales in the epilogue) on the tile
+    and the 256x256 kernels: equal to a torch fp32 matmul of the dequantised e4m3 operands up to fp32
+    summation order; split-K slabs, bf16 and gelu*up epilogues."""
+    from pghip import ops
+    from pghip.weights import quant_rows_fp8
+    A, W = rnd(M, K, seed=52), rnd(N, K, scale=1 / math.sqrt(K), seed=53)
+    bias = torch.randn(N).cuda()
+    a8, sa = ops.quant_fp8(A)
+    w8, sw = quant_rows_fp8(W)
+    ref = _deq(a8, sa) @ _deq(w8, sw).t()
+    out = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    ops.gemm8(a8, sa, w8, sw, out, epi=ops.EPI_F32, bias=bias)
+    # (the reference rounds every dequantised operand to fp32; the kernel scales the exact e4m3 products once)
+    assert err(out, ref + bias) < 5e-5
+    part = torch.empty(3, M, N, dtype=torch.float32, device="cuda")
+    ops.gemm8(a8, sa, w8, sw, part, epi=ops.EPI_F32, bias=bias, ksplit=3)
+    assert err(part.sum(0), ref + bias) < 5e-5
+    outb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(a8, sa, w8, sw, outb, epi=ops.EPI_BF16, bias=bias)
+    assert err(outb, ref + bias) < 1e-2
+    h = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(a8, sa, w8, sw, h, epi=ops.EPI_BF16_GELU_MUL)
+    g = ref.view(M, N // 32, 2, 16)
+    want = (torch.nn.functional.gelu(g[:, :, 0], approximate="tanh") * g[:, :, 1]).reshape(M, N // 2)
+    assert err(h, want) < 1e-2
+    # and the quantisation error against the bf16 product stays at the e4m3 level
+    assert err(out - bias, A.float() @ W.float().t()) < 0.1
