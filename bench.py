@@ -143,6 +143,9 @@ def main():
     ap.add_argument("--comm", default="xgmi", choices=["xgmi", "rccl"],
                     help="TP all-reduce: pg_allreduce_xgmi for decode-size slabs (RCCL/gloo beyond its buffer), "
                     "or the process group's collective only")
+    ap.add_argument("--fp8", action="store_true",
+                    help="Gemma linears as fp8 e4m3 (per-channel / per-row scales) for GEMMs over 16 rows, as BASELINE "
+                    "configs[4]")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
                     "instead of greedy, as BASELINE configs[3]")
@@ -173,10 +176,10 @@ def main():
     if tp > 1:
         from pghip.tp import TPComm, XgmiComm
         comm = XgmiComm() if args.comm == "xgmi" else TPComm()
-        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=tp),
-                                     comm=comm)
+        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=tp,
+                                                                fp8=args.fp8), comm=comm)
     else:
-        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=args.fp8))
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: weights generated+packed in {time.perf_counter() - t0:.1f}s "
         f"({eng.w.nbytes() / 1e9:.2f} GB)")
@@ -277,7 +280,7 @@ def main():
     torch.cuda.synchronize()
     prefill_ms = ev[0].elapsed_time(ev[1]) / 3
     decode_ms_tok = ev[2].elapsed_time(ev[3]) / (T - 1)
-    step_bytes = eng.w.decode_weight_bytes()
+    step_bytes = eng.w.decode_weight_bytes_fp8() if args.fp8 and B > 16 else eng.w.decode_weight_bytes()
     kv_bytes = B * (L + T // 2) * eng.w.t_layers * 2 * eng.w.kv_heads * eng.w.head_dim * 2
     decode_hbm = (step_bytes + kv_bytes) / (decode_ms_tok / 1e3) / 1e9
     pf_flops = prefill_flops(cfg, B, L)
@@ -298,6 +301,8 @@ def main():
 
     baseline_ref = {("pt-224", 1): "BASELINE.json configs[1]", ("pt-448", 16): "BASELINE.json configs[2]"}.get(
         (args.config, B), "not a BASELINE.json config")
+    if args.config == "pt-896" and B == 32 and args.fp8:
+        baseline_ref = f"BASELINE.json configs[4] shapes (fp8) at {'TP=%d' % tp if tp > 1 else 'one GPU'}"
     if tp == 2 and args.sample and args.config in ("pt-224", "mix-224"):
         baseline_ref = "BASELINE.json configs[3] (mix-224 = the pt-224 architecture)"
     if rank == 0:
@@ -305,7 +310,8 @@ def main():
             "metric": BASELINE_METRIC,
             "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
-            "scaling": "weak" if tp == 1 else "strong", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random-init weights of the "
+            "scaling": "weak" if tp == 1 else "strong", "vs_baseline": None,
+            "dtype": "fp8-e4m3 Gemma linears (>16 rows), bf16 elsewhere" if args.fp8 else "bf16", "data": "synthetic (random-init weights of the "
             "PaliGemma-3B architecture, name-seeded; random 224x224 image; 8-token prompt)",
             "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
                                    f"{T} {'top-p' if args.sample else 'greedy'} tokens ({baseline_ref})",

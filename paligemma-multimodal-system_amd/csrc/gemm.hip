@@ -533,7 +533,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * 4 * HALF;
-#if PG_G256_PREFETCH
+    if constexpr (PG_G256_PREFETCH && !F8) {   // (fp8: the early reads would spill)
     // the reads of phases 1-3 are issued one phase early, ahead of the current phase's MFMAs (tile t is
     // retired for every wave from phase 0 on; each half is still restaged only after its last read)
     read_a(buf, fa0);
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_s_barrier();
     if (t + 2 < nk) stage(1, t + 2);
     mma(1, 0, fa1, fb0);
-#else
+    } else {
     // phase 0: quadrant (rows 0-63, cols 0-31) from A0, B0; restage B0 of tile t+1
     read_a(buf, fa0);
     read_b(buf + 2 * HALF, fb0);
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     read_b(buf + 2 * HALF, fb0);
     if (t + 2 < nk) stage(1, t + 2);
     mma(1, 0, fa0, fb0);
-#endif
+    }
     if (t + 2 < nk) wait_vm(6); else wait_vm(0);
     __builtin_amdgcn_s_barrier();
   }
@@ -635,6 +635,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #endif
 #ifndef PG_AO_SPLITS_PER_WG
 #define PG_AO_SPLITS_PER_WG 1   // pg_attn_oproj: attention splits per workgroup (one wave each, <= 4)
+#endif
+#ifndef PG_F8_G256
+#define PG_F8_G256 0            // fp8 GEMMs on the 256x256 kernel: it spills at fp8 (2x slower than the 128x128 tile kernel)
 #endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
@@ -1185,7 +1188,7 @@ template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
-  if (t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
+  if ((PG_F8_G256 || !F8) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;
     hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG, F8>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
                        (e.M + 255) / 256, (e.N + 255) / 256, e);

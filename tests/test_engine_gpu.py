@@ -224,3 +224,49 @@ def test_batched_generation_per_row_eos(tiny, golden):
     for b in range(2):
         assert out[b, : len(single[b])].tolist() == single[b]
         assert (out[b, len(single[b]):] == 0).all()
+
+
+# ---------------------------------------------------------------- fp8 Gemma linears (BASELINE configs[4])
+TOL_FP8 = 0.12  # e4m3 operands (3 mantissa bits), per-row / per-channel scales: looser than bf16 (measured 0.086)
+
+
+@pytest.fixture(scope="module")
+def tiny_fp8():
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    from pghip import configs, engine, synthetic, weights
+    cfg = configs.TINY
+    return engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__,
+                                                             fp8=True))
+
+
+def test_tiny_fp8_prefill_and_batched_decode_vs_oracle(tiny_fp8, golden):
+    """fp8 engine (Gemma q|k|v, o, gate/up, down as PG_FP8 GEMMs for > 16 rows): prefill logits of the golden
+    prompt replicated to a batch of 20 (every GEMM on the fp8 path), then teacher-forced decode steps at
+    B = 20 (fp8 tile GEMMs) against the fp32 oracle; greedy ids must agree where the oracle's top-1/top-2
+    margin exceeds 0.5 logits."""
+    from oracle import configs as ocfg, synth, paligemma_oracle as O
+    eng = tiny_fp8
+    orc = O.PaliGemmaOracle(ocfg.TINY, synth.generate_state_dict(ocfg.TINY), recompute_vision=False)
+    g = golden("tiny")
+    ids_np = g["b1_input_ids"]
+    steps, B = 8, 20
+    ref_ids, ref_logits = O.generate(orc, ids_np, g["b1_pixel_values"], np.ones_like(ids_np), steps,
+                                     stop_token=None, record_logits=True)
+    ids = torch.from_numpy(ids_np).cuda().repeat(B, 1)
+    px = torch.from_numpy(g["b1_pixel_values"]).cuda().repeat(B, 1, 1, 1)
+    cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), steps)
+    worst = err(logits[:1].cpu().numpy(), ref_logits[0])
+    assert worst < TOL_FP8, worst
+    assert torch.equal(logits[0], logits[B - 1])                         # rows are independent
+    st = eng.decode_state(B, cache, nxt, steps)
+    for t in range(1, steps):
+        st["ids"].fill_(ref_ids[t - 1])
+        lg = eng.decode_step(st, cache, feats, dict(do_sample=False))
+        e = err(lg[:1].cpu().numpy(), ref_logits[t])
+        worst = max(worst, e)
+        assert e < TOL_FP8, (t, e)
+        top = np.sort(ref_logits[t][0])[::-1]
+        if top[0] - top[1] > 0.5:
+            assert int(st["ids"][0]) == ref_ids[t], t
+    print(f"fp8 tiny worst scaled logit error {worst:.4f}")
