@@ -192,6 +192,11 @@ int pg_prefetch(const void* p, long bytes, int wgs, int policy, hipStream_t stre
 /* fp8 row quantisation feeding PG_FP8 GEMMs: q[m][k] = e4m3(x[m][k] / scale[m]), scale[m] = max|x[m][:]| / 448
  * (1 for an all-zero row).  x bf16 (row stride ldx), q bytes (row stride ldq).  K, ldx, ldq multiples of 8. */
 int pg_quant_fp8(const void* x, int ldx, int M, int K, void* q, int ldq, float* scale, hipStream_t stream);
+/* pg_norm_residual with y quantised as pg_quant_fp8 of its bf16 value: q uint8 [M_out][ldq], scale [M_out]
+ * (one launch feeding a PG_FP8 GEMM; GemmaRMSNorm modeling_gemma.py:165-182 / nn.LayerNorm). */
+int pg_norm_residual_fp8(float* resid, const float* partials, int nsplit, int M_part, const float* w,
+                         const float* b, void* q, int ldq, float* scale, const int* row_map, int M_out,
+                         int H, int mode, float eps, int write_resid, hipStream_t stream);
 
 /* ---- one-shot all-reduce over xGMI (the reference is single-device, so this
  * replaces nothing there -- it is the tensor-parallel exchange of the Gemma decoder's o_proj / down_proj

@@ -359,7 +359,8 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
 //         -> the two ds_read_b64 of a PV fragment are conflict-free
 // Per block a wave does 4 x KS S^T MFMAs, an online softmax on 16 scores per lane (the rescale of O is
 // skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
-// V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row).
+// V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row);
+// K dims past D (D < DP) are never read from memory.
 template <int DP, int DT, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   constexpr int KS = DP / 32;
@@ -400,7 +401,9 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     for (int i = wave; i < KINS; i += WAVES) {
       const int kg = i / (NCH / 4), cq = i % (NCH / 4);
       const int ch = 4 * cq + (lane >> 4), key = 16 * kg + (lane & 15);
-      const bf16_t* src = kbase + (long)min(kb + key, Lkv - 1) * a.k_rs + ch * 8;
+      // chunks past D (D < DP) re-read chunk 0: the matching q dims are zero, and 0 * (finite K) = 0, whereas
+      // the bytes past a head's D may be another tensor's never-written memory (NaN * 0 = NaN)
+      const bf16_t* src = kbase + (long)min(kb + key, Lkv - 1) * a.k_rs + (ch * 8 < D ? ch * 8 : 0);
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(kimg + i * 1024), 16, 0, 0);
     }
     for (int i = wave; i < VINS; i += WAVES) {

@@ -11,6 +11,9 @@
 
 #define NORM_MAXV 4   // float4 per thread -> H <= 4096
 
+// Q8: y goes out as fp8 e4m3 bytes (out = uint8 [M][ldo]) with its row scale in out_f32[orow] (the
+// pg_quant_fp8 rule applied to the bf16-rounded y, so the bytes equal quantising the bf16 output).
+template <bool Q8>
 __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ resid, const float* __restrict__ partials,
                                                             int nsplit, int M_part, const float* __restrict__ w,
                                                             const float* __restrict__ b, bf16_t* __restrict__ out,
@@ -59,6 +62,7 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
       for (int j = 0; j < 4; ++j) q += v[i][j] * v[i][j];
     rstd = rsqrtf(block_sum(q, red) / (float)H + eps);
   }
+  float amax = 0.f;
 #pragma unroll
   for (int i = 0; i < NORM_MAXV; ++i) {
     const int c = threadIdx.x + i * 256;
@@ -73,6 +77,14 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
 #pragma unroll
         for (int j = 0; j < 4; ++j) y[j] = (v[i][j] * rstd) * (1.0f + wv[j]);
       }
+      if constexpr (Q8) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[i][j] = __uint_as_float((uint32_t)f2bf(y[j]) << 16);     // the bf16 value the GEMM would have read
+          amax = fmaxf(amax, fabsf(v[i][j]));
+        }
+        continue;
+      }
       if (out) {
         u32x2 p;
         p[0] = pack_bf2(y[0], y[1]);
@@ -80,6 +92,29 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
         *(u32x2*)(out + (size_t)orow * ldo + c * 4) = p;
       }
       if (out_f32) ((f32x4*)(out_f32 + (size_t)orow * H))[c] = y;
+    }
+  }
+  if constexpr (Q8) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const float sc = amax > 0.f ? amax / 448.f : 1.f;
+    if (threadIdx.x == 0) out_f32[orow] = sc;
+    uint8_t* q = (uint8_t*)out + (size_t)orow * ldo;
+#pragma unroll
+    for (int i = 0; i < NORM_MAXV; ++i) {
+      const int c = threadIdx.x + i * 256;
+      if (c < H4) {
+        float t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = fminf(fmaxf(v[i][j] / sc, -448.f), 448.f);
+        int wq = __builtin_amdgcn_cvt_pk_fp8_f32(t[0], t[1], 0, false);
+        wq = __builtin_amdgcn_cvt_pk_fp8_f32(t[2], t[3], wq, true);
+        *(uint32_t*)(q + c * 4) = (uint32_t)wq;
+      }
     }
   }
 }
@@ -92,8 +127,23 @@ extern "C" int pg_norm_residual(float* resid, const float* partials, int nsplit,
   PG_REQUIRE(M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV);
   PG_REQUIRE(mode == 1 || b != nullptr);
   PG_REQUIRE(nsplit == 0 || partials != nullptr);
-  hipLaunchKernelGGL(norm_residual_kernel, dim3(M_out), dim3(256), 0, stream, resid, partials, nsplit, M_part, w, b,
-                     (bf16_t*)out, ldo, out_f32, row_map, H, mode, eps, write_resid);
+  hipLaunchKernelGGL(norm_residual_kernel<false>, dim3(M_out), dim3(256), 0, stream, resid, partials, nsplit, M_part,
+                     w, b, (bf16_t*)out, ldo, out_f32, row_map, H, mode, eps, write_resid);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
+// The same normalisation with y quantised to fp8 e4m3 for a PG_FP8 GEMM: q uint8 [M_out][ldq], scale [M_out]
+// (pg_quant_fp8 of the bf16 output, fused: one launch and no bf16 round trip).  H % 4 == 0, ldq % 4 == 0.
+extern "C" int pg_norm_residual_fp8(float* resid, const float* partials, int nsplit, int M_part, const float* w,
+                                    const float* b, void* q, int ldq, float* scale, const int* row_map, int M_out,
+                                    int H, int mode, float eps, int write_resid, hipStream_t stream) {
+  PG_REQUIRE(M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV && q != nullptr && scale != nullptr &&
+             ldq >= H && ldq % 4 == 0);
+  PG_REQUIRE(mode == 1 || b != nullptr);
+  PG_REQUIRE(nsplit == 0 || partials != nullptr);
+  hipLaunchKernelGGL(norm_residual_kernel<true>, dim3(M_out), dim3(256), 0, stream, resid, partials, nsplit, M_part,
+                     w, b, (bf16_t*)q, ldq, scale, row_map, H, mode, eps, write_resid);
   PG_LAUNCH_CHECK();
   return 0;
 }

@@ -193,11 +193,11 @@ class PaliGemmaEngine:
             taps.append(x_resid.clone())
         kvd = nkv * hd
         for i, Lw in enumerate(w.tl):
-            ops.norm_residual(x_resid, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            xin = self._norm(x_resid, Lw["in_w"], part, ns, xn, T)
             # q|k|v projection + RoPE + KV-cache append in one GEMM (modeling_gemma.py:274-302)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=0,
                                 kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
-            self._lin(xn, Lw, "qkv", qb, ops.EPI_QKV_ROPE, T, fa=fa)
+            self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, T, fa=fa)
             ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
@@ -205,8 +205,8 @@ class PaliGemmaEngine:
                           mask_rs=(mask.stride(-2) if mask is not None else 0))
             self._lin(attn, Lw, "o", part, ops.EPI_F32, T, ksplit=s_o)
             self._allreduce(part[:s_o])
-            ops.norm_residual(x_resid, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=s_o, out=xn)
-            self._lin(xn, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
+            xin = self._norm(x_resid, Lw["post_w"], part, s_o, xn, T)
+            self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
             self._lin(h, Lw, "down", part, ops.EPI_F32, T, ksplit=s_d)
             self._allreduce(part[:s_d])
             ns = s_d
@@ -233,6 +233,9 @@ class PaliGemmaEngine:
         """One Gemma linear: bf16 (fragment-packed W) or, with fp8 weights and M > 16, the activation rows
         quantised to e4m3 (pg_quant_fp8) feeding the PG_FP8 GEMM with the per-channel weight scales."""
         w = self.w
+        if isinstance(x, tuple):        # already quantised (_norm)
+            x8, xs = x
+            return ops.gemm8(x8, xs, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa)
         if self._fp8_rows(M):
             K = x.shape[1]
             x8 = self._buf(f"x8_{K}", (M, K), torch.uint8)
@@ -242,6 +245,17 @@ class PaliGemmaEngine:
         if fa is not None:
             return ops.gemm_fused(x, Lw[name + "_w"], out, fa, epi=epi | w.wflag, M=M)
         return ops.gemm(x, Lw[name + "_w"], out, epi=epi | w.wflag, ksplit=ksplit)
+
+    def _norm(self, resid: torch.Tensor, norm_w: torch.Tensor, part, nsplit: int, xn: torch.Tensor, M: int):
+        """Gemma RMSNorm of the residual (+ split-K partials) feeding a linear: bf16 rows, or fp8 rows with
+        their scales (one launch, pg_norm_residual_fp8) when that linear runs on the fp8 path."""
+        if self._fp8_rows(M):
+            H = resid.shape[-1]
+            x8 = self._buf(f"x8_{H}", (M, H), torch.uint8)
+            xs = self._buf(f"xs_{H}", (M,), torch.float32)
+            return ops.norm_residual_fp8(resid, norm_w, x8, xs, mode=ops.NORM_RMS, partials=part, nsplit=nsplit)
+        ops.norm_residual(resid, norm_w, mode=ops.NORM_RMS, partials=part, nsplit=nsplit, out=xn)
+        return xn
 
     def _allreduce(self, t: torch.Tensor):
         if self.tp > 1:
@@ -297,7 +311,7 @@ class PaliGemmaEngine:
         h = self._buf("d_h", (B, I), torch.bfloat16)
         so, sd = self.split_o, self.split_down
         part = self._buf("d_part", (max(so, sd), B, H), torch.float32)
-        SK = self.DECODE_SPLIT_KEYS
+        SK = self._split_keys(B, cache.Smax)
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
         dt = (hd + 15) // 16 * 16
         part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
@@ -308,7 +322,7 @@ class PaliGemmaEngine:
         ns = 0
         if B > self.FUSE_MAX_B:
             ns = self._decode_layers_unfused(st, cache, res_a, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t,
-                                             sin_t)
+                                             sin_t, SK)
         if B <= self.FUSE_MAX_B and self.tp == 1 and self.USE_FIN:
             xq, ss, tiles = self._decode_layers_fin(st, cache, res_a, qb, h, part, part_o, part_ml, nsplit, dt,
                                                     cos_t, sin_t)
@@ -422,7 +436,18 @@ class PaliGemmaEngine:
             ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
         return xq, ss_d, tiles
 
-    def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
+    def _split_keys(self, B: int, Smax: int) -> int:
+        """Keys per decode-attention split: 32 (one MFMA block) at small batch; at B > FUSE_MAX_B (separate
+        merge kernel) whole multiples of 32 such that B * splits stays near 1024 waves -- fewer (O, m, l)
+        partials to write and merge once the batch alone fills the chip."""
+        SK = self.DECODE_SPLIT_KEYS
+        if B <= self.FUSE_MAX_B:
+            return SK
+        blocks = (Smax + SK - 1) // SK
+        return SK * max(1, min(8, (B * blocks) // 1024))
+
+    def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t,
+                               SK=None):
         """Decode layers for B > FUSE_MAX_B: the RMSNorm and the split-KV merge run once as their own
         kernels (fused into every GEMV workgroup they would be recomputed B-fold per workgroup)."""
         w = self.w
@@ -433,21 +458,21 @@ class PaliGemmaEngine:
         attn = self._buf("d_attn", (B, nh * hd), torch.bfloat16)
         ns = 0
         for i, Lw in enumerate(w.tl):
-            ops.norm_residual(res, Lw["in_w"], mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn)
+            xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv)
-            self._lin(xn, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
+            self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=self.DECODE_SPLIT_KEYS, nsplit=nsplit, part_o=part_o,
-                          part_ml=part_ml)
+                          scale=1.0 / math.sqrt(hd), split_keys=SK or self.DECODE_SPLIT_KEYS, nsplit=nsplit,
+                          part_o=part_o, part_ml=part_ml)
             ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
             self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
             self._allreduce(part[:so])
-            ops.norm_residual(res, Lw["post_w"], mode=ops.NORM_RMS, partials=part, nsplit=so, out=xn)
-            self._lin(xn, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
+            xin = self._norm(res, Lw["post_w"], part, so, xn, B)
+            self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
             self._lin(h, Lw, "down", part, ops.EPI_F32, B, ksplit=sd)
             self._allreduce(part[:sd])
             ns = sd

@@ -190,6 +190,20 @@ def norm_residual(resid: torch.Tensor, w: torch.Tensor, *, b: Optional[torch.Ten
               _p(row_map), M_out, H, mode, float(eps), int(write_resid), _s())
 
 
+def norm_residual_fp8(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, scale: torch.Tensor, *,
+                      b: Optional[torch.Tensor] = None, mode: int = NORM_RMS, eps: float = 1e-6,
+                      partials: Optional[torch.Tensor] = None, nsplit: int = 0, write_resid: bool = True):
+    """norm_residual with the output quantised to fp8 e4m3 rows (q uint8 [M][H], scale fp32 [M]) for a
+    PG_FP8 GEMM; the bytes equal quant_fp8 of the bf16 output (pg_norm_residual_fp8)."""
+    _chk(resid, torch.float32, "resid")
+    M, H = resid.shape[-2], resid.shape[-1]
+    if q.dtype != torch.uint8 or q.stride(-1) != 1 or q.shape[-1] < H or scale.numel() < M:
+        raise ValueError("pghip.norm_residual_fp8: bad output buffers")
+    _lib.call("pg_norm_residual_fp8", _p(resid), _p(partials), nsplit, M, _p(w), _p(b), _p(q), q.stride(-2),
+              _p(scale), None, M, H, mode, float(eps), int(write_resid), _s())
+    return q, scale
+
+
 def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lq, Lkv, Hq, Hkv, D,
               scale, mask=None, mask_bs=0, mask_rs=0, lkv_dev=None, split_keys=0, nsplit=0, part_o=None,
               part_ml=None):

@@ -519,3 +519,24 @@ def test_gemm_fp8_matches_fp32_matmul_of_dequantised_operands(M, N, K):
     assert err(h, want) < 1e-2
     # and the quantisation error against the bf16 product stays at the e4m3 level
     assert err(out - bias, A.float() @ W.float().t()) < 0.1
+
+
+@pytest.mark.parametrize("M,H,nsplit", [(5, 2048, 0), (300, 2048, 3), (17, 1152, 1)])
+def test_norm_residual_fp8_equals_quantised_bf16_output(M, H, nsplit):
+    """pg_norm_residual_fp8 == pg_quant_fp8(pg_norm_residual bf16 output), bytes and scales; the residual
+    update is the same."""
+    from pghip import ops
+    g = torch.Generator().manual_seed(61)
+    resid = torch.randn(M, H, generator=g).cuda()
+    part = torch.randn(max(nsplit, 1), M, H, generator=g).cuda() * 0.1
+    w = torch.randn(H, generator=g).cuda() * 0.1
+    r1, r2 = resid.clone(), resid.clone()
+    xn = torch.empty(M, H, dtype=torch.bfloat16, device="cuda")
+    ops.norm_residual(r1, w, mode=ops.NORM_RMS, partials=part, nsplit=nsplit, out=xn)
+    q_ref, s_ref = ops.quant_fp8(xn)
+    q = torch.empty(M, H, dtype=torch.uint8, device="cuda")
+    s = torch.empty(M, dtype=torch.float32, device="cuda")
+    ops.norm_residual_fp8(r2, w, q, s, mode=ops.NORM_RMS, partials=part, nsplit=nsplit)
+    assert torch.equal(r1, r2)
+    assert torch.equal(s, s_ref)
+    assert torch.equal(q, q_ref)
