@@ -538,14 +538,29 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   __syncthreads();
   if (threadIdx.x == 0) inv_den = 1.0f / (red[0] + red[1] + red[2] + red[3]);
   __syncthreads();
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float num = 0.f;
-#pragma unroll 8
-    for (int s2 = 0; s2 < nsplit; ++s2) {
+  // thread (sg, dq): dims 4dq..4dq+3, splits sg, sg+4, ... (16-B loads, 4 independent streams per dim
+  // group, no branch around a load); the four split groups are summed in LDS
+  const int dq = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  f32x4 num = {0.f, 0.f, 0.f, 0.f};
+  if (4 * dq < D) {
+    const float* po = part_o + ((long)bk * nsplit * 16 + row) * DTW + 4 * dq;
+#pragma unroll 4
+    for (int s2 = sg; s2 < nsplit; s2 += 4) {
       const float wv = wsh[s2];
-      if (wv != 0.f) num += wv * part_o[(((long)bk * nsplit + s2) * 16 + row) * DTW + d];
+      const f32x4 pv = *(const f32x4*)(po + (long)s2 * 16 * DTW);
+      num += wv != 0.f ? wv * pv : f32x4{0.f, 0.f, 0.f, 0.f};   // empty splits hold no partials
     }
-    o[(long)b * o_rs + (long)(kvh * G + row) * D + d] = f2bf(num * inv_den);
+  }
+  __shared__ f32x4 part_sum[3][64];
+  if (sg > 0) part_sum[sg - 1][dq] = num;
+  __syncthreads();
+  if (sg == 0 && 4 * dq < D) {
+    num += part_sum[0][dq] + part_sum[1][dq] + part_sum[2][dq];
+    num *= inv_den;
+    u32x2 pk;
+    pk[0] = pack_bf2(num[0], num[1]);
+    pk[1] = pack_bf2(num[2], num[3]);
+    *(u32x2*)(o + (long)b * o_rs + (long)(kvh * G + row) * D + 4 * dq) = pk;
   }
 }
 
@@ -623,6 +638,7 @@ extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B,
                                void* o, long o_rs, hipStream_t stream) {
   PG_REQUIRE(Hq % Hkv == 0 && Hq / Hkv <= 16 && nsplit <= 256);
   const int DT = (D + 15) / 16;
+  PG_REQUIRE(D <= 256 && D % 4 == 0 && o_rs % 4 == 0 && ((uintptr_t)o & 7) == 0 && nsplit <= 256);
   hipLaunchKernelGGL(attn_combine_kernel, dim3(B * Hq), dim3(256), 0, stream, part_o, part_ml, nsplit, Hq / Hkv,
                      Hkv, D, DT * 16, (bf16_t*)o, o_rs);
   PG_LAUNCH_CHECK();

@@ -943,16 +943,31 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : 0) * lda : nullptr;
   // PRO 4 (M <= 2): wave 0 loads the producer's per-tile sums of squares before the weight stream (all
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
-  float ssv[4] = {0.f, 0.f, 0.f, 0.f};
+  // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
+  // own row, so the row total is a reduction over the 4 lane groups
+  constexpr int SSL = (PRO == 4 && NT == 2) ? 16 : 4;
+  float ssv[SSL];
+#pragma unroll
+  for (int k = 0; k < SSL; ++k) ssv[k] = 0.f;
   if constexpr (PRO == 4) {
     if (wave == 0) {
-      const int lpr = M == 1 ? 64 : 32;
-      const int rr = min(lane / lpr, M - 1);
+      if (NT == 2 && M > 2) {
+        const int rr = min(r, M - 1);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int i = lane % lpr + k * lpr;
-        const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
-        ssv[k] = i < e.f.ss_n ? v : 0.f;
+        for (int k = 0; k < SSL; ++k) {
+          const int i = g + 4 * k;
+          const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
+          ssv[k] = i < e.f.ss_n ? v : 0.f;
+        }
+      } else {
+        const int lpr = M == 1 ? 64 : 32;
+        const int rr = min(lane / lpr, M - 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int i = lane % lpr + k * lpr;
+          const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
+          ssv[k] = i < e.f.ss_n ? v : 0.f;
+        }
       }
     }
   }
@@ -1061,10 +1076,17 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     for (int t = 0; t < NT; ++t) acc[t] *= rs;
   }
   if constexpr (PRO == 4) {
-    const int lpr = M == 1 ? 64 : 32;
-    float ss = ssv[0] + ssv[1] + ssv[2] + ssv[3];
-    for (int o = 1; o < lpr; o <<= 1) ss += __shfl_xor(ss, o, 64);
-    ss = __shfl(ss, (m < M ? m : 0) * lpr, 64);
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < SSL; ++k) ss += ssv[k];
+    if (NT == 2 && M > 2) {
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+    } else {
+      const int lpr = M == 1 ? 64 : 32;
+      for (int o = 1; o < lpr; o <<= 1) ss += __shfl_xor(ss, o, 64);
+      ss = __shfl(ss, (m < M ? m : 0) * lpr, 64);
+    }
     const float rs = rsqrtf(ss / (float)K + e.f.eps);
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] *= rs;
@@ -1291,8 +1313,10 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
     PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 4);
   }
   if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
-  if (f.pro_mode == 4) PG_REQUIRE(M <= 2 && ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_n <= 256 &&
-                                  (M == 1 || f.ss_n <= 128) && f.ss_ld >= f.ss_n);
+  // (M > 4 runs two 16-row tiles per workgroup: the per-row entries are loaded 16 per lane)
+  if (f.pro_mode == 4) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
+                                  ((M <= 2 && f.ss_n <= 256 && (M == 1 || f.ss_n <= 128)) ||
+                                   (M > 4 && M <= 16 && f.ss_n <= 64)));
   if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
   if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
   if (f.pro_mode == 2 || f.pro_mode == 5)
@@ -1303,7 +1327,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                          N == (f.q_heads + 2 * f.kv_heads) * f.head_dim);
   if (f.pro_mode == 3) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && f.ss_in && f.ss_n > 0 &&
                                   f.ss_ld >= f.ss_n && K % 4 == 0);
-  if (epi == PG_EPI_F32_FIN) PG_REQUIRE(M <= 4 && ksplit <= 8 && (f.fin_x == nullptr || f.norm_w != nullptr) && f.fin_cnt && f.fin_resid && f.ss_out && f.ss_ld >= (N + 15) / 16 &&
+  if (epi == PG_EPI_F32_FIN) PG_REQUIRE(M <= 16 && ksplit <= 8 && (f.fin_x == nullptr || f.norm_w != nullptr) && f.fin_cnt && f.fin_resid && f.ss_out && f.ss_ld >= (N + 15) / 16 &&
                                         ldc == N);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);

@@ -66,6 +66,8 @@ class PaliGemmaEngine:
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
+    DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
+    FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
     FUSE_ATTN_O = False     # with USE_FIN: the split-KV attention inside the o_proj launch (pg_attn_oproj): correct,
                             # measured 1.31 vs 1.19 ms/token (the fused GEMV drops to 1 wave/SIMD; 252 pollers)
@@ -320,21 +322,23 @@ class PaliGemmaEngine:
                         image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
                         normalizer=float(w.hidden ** 0.5))
         ns = 0
-        if B > self.FUSE_MAX_B:
+        fin = self.tp == 1 and self.USE_FIN and (B <= self.FUSE_MAX_B or self.FIN_MIN_B <= B <= 16) and \
+            not self._fp8_rows(B)
+        if B > self.FUSE_MAX_B and not fin:
             ns = self._decode_layers_unfused(st, cache, res_a, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t,
                                              sin_t, SK)
-        if B <= self.FUSE_MAX_B and self.tp == 1 and self.USE_FIN:
-            xq, ss, tiles = self._decode_layers_fin(st, cache, res_a, qb, h, part, part_o, part_ml, nsplit, dt,
-                                                    cos_t, sin_t)
+        if fin:
+            xq, ss, tiles, n_ss = self._decode_layers_fin(st, cache, res_a, qb, h, part, part_o, part_ml, nsplit, dt,
+                                                          cos_t, sin_t, SK)
             # final RMSNorm folded into the lm_head GEMV: x' = resid*(1+w) from the last down_proj, rstd on the outputs
             logits = self._buf("d_logits", (B, w.vocab_local_pad), torch.float32)
-            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
             ops.gemm_fused(xq, w.lm_w, logits, fa, epi=ops.EPI_F32 | w.wflag, M=B, bias=w.lm_bias)
             logits = logits[:, :w.vocab]
             if sampler is not None:
                 self.sample(logits, st, sampler, advance=True)
             return logits
-        for i, Lw in enumerate(w.tl if B <= self.FUSE_MAX_B else ()):
+        for i, Lw in enumerate(w.tl if B <= self.FUSE_MAX_B else ()):      # (TP / USE_FIN off, B <= FUSE_MAX_B)
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
                                 norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
                                 rows_per_batch=1, slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i],
@@ -381,24 +385,30 @@ class PaliGemmaEngine:
             self._ws[name] = t
         return t
 
-    def _decode_layers_fin(self, st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t):
+    def _decode_layers_fin(self, st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t, SK=None):
         """Decode layers (single rank, B <= FUSE_MAX_B) in 5 launches with in-kernel split-K finalisation:
         o_proj and down_proj add their split-K slabs into the residual in place (the last-arriving split of
         each 16-column tile), and write x' = bf16(resid*(1+w_next)) plus per-tile sums of squares; the next
         GEMV (gate/up, the next layer's qkv, finally the lm_head) reads x' like a plain activation and
         scales its outputs by rstd (RMSNorm: W.(x*rstd*(1+w)) = rstd * W.(x*(1+w))).
-        Returns (x', sums of squares, tiles) of the final norm for the lm_head."""
+        At B > FUSE_MAX_B (up to 16 rows) the split-KV merge runs as its own kernel (folded into every o_proj
+        workgroup it would be recomputed per workgroup) and the GEMVs run two 16-row tiles per workgroup, so
+        the sums of squares come one per tile pair.
+        Returns (x', sums of squares, their row stride, entries per row) of the final norm for the lm_head."""
         w = self.w
         B = st["ids"].numel()
         H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
         so, sd = self.split_o, self.split_down
         tiles = (H + 15) // 16
+        n_ss = tiles if B <= 4 else (tiles + 1) // 2         # one entry per GEMV workgroup (M > 4: tile pairs)
+        merge_in_gemv = B <= self.FUSE_MAX_B
+        attn = None if merge_in_gemv else self._buf("d_attn", (B, nh * hd), torch.bfloat16)
         cnt = self._zeros("d_fin_cnt", (tiles,), torch.int32)
         ss_o = self._buf("d_ss_o", (B, tiles), torch.float32)
         ss_d = self._buf("d_ss_d", (B, tiles), torch.float32)
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
-        SK = self.DECODE_SPLIT_KEYS
+        SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
@@ -409,20 +419,27 @@ class PaliGemmaEngine:
                                     **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=tiles, eps=1e-6, **rope)
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
-            fused = self.FUSE_ATTN_O and nsplit <= 16
+            fused = self.FUSE_ATTN_O and nsplit <= 16 and merge_in_gemv
             if not fused:
                 ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                               cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                               B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                               scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
                               part_ml=part_ml)
+            if not merge_in_gemv:
+                ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+                fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
+                                    norm_w=Lw["post_w"])
+                ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_INLINE if fused else ops.PRO_ATTN_COMBINE, part_o=part_o,
                                 part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv,
                                 slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles,
                                 fin_x=xq, norm_w=Lw["post_w"])
-            if fused:   # attention computed by the first workgroups of the o_proj GEMV (one launch)
+            if not merge_in_gemv:
+                pass
+            elif fused:   # attention computed by the first workgroups of the o_proj GEMV (one launch)
                 ops.attn_oproj(qb, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd, cache.vt[i], kvd * cache.Smax,
                                hd * cache.Smax, cache.Smax, Lw["o_w"], part, fa, self._zeros("d_attn_sync", (4,),
                                torch.int32), B=B, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
@@ -430,21 +447,21 @@ class PaliGemmaEngine:
             else:
                 ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=tiles, eps=1e-6)
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
             ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
             fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
             ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
-        return xq, ss_d, tiles
+        return xq, ss_d, tiles, n_ss
 
     def _split_keys(self, B: int, Smax: int) -> int:
         """Keys per decode-attention split: 32 (one MFMA block) at small batch; at B > FUSE_MAX_B (separate
-        merge kernel) whole multiples of 32 such that B * splits stays near 1024 waves -- fewer (O, m, l)
+        merge kernel) whole multiples of 32 such that B * splits stays near DECODE_SPLIT_TARGET -- fewer (O, m, l)
         partials to write and merge once the batch alone fills the chip."""
         SK = self.DECODE_SPLIT_KEYS
         if B <= self.FUSE_MAX_B:
             return SK
         blocks = (Smax + SK - 1) // SK
-        return SK * max(1, min(8, (B * blocks) // 1024))
+        return SK * max(1, min(8, (B * blocks) // self.DECODE_SPLIT_TARGET))
 
     def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t,
                                SK=None):

@@ -20,6 +20,7 @@ ap.add_argument("--split-o", type=int, default=None)
 ap.add_argument("--split-down", type=int, default=None)
 ap.add_argument("--split-keys", type=int, default=None)
 ap.add_argument("--batch", type=int, default=1)
+ap.add_argument("--split-target", type=int, default=None)
 ap.add_argument("--no-fuse-ao", action="store_true", help="attention as its own kernel (not inside o_proj)")
 a = ap.parse_args()
 
@@ -35,6 +36,8 @@ if a.split_down:
     eng.split_down = a.split_down
 if a.split_keys:
     eng.DECODE_SPLIT_KEYS = a.split_keys
+if a.split_target:
+    eng.DECODE_SPLIT_TARGET = a.split_target
 if a.no_fuse_ao:
     eng.FUSE_ATTN_O = False
 B = a.batch

@@ -270,3 +270,36 @@ def test_tiny_fp8_prefill_and_batched_decode_vs_oracle(tiny_fp8, golden):
         if top[0] - top[1] > 0.5:
             assert int(st["ids"][0]) == ref_ids[t], t
     print(f"fp8 tiny worst scaled logit error {worst:.4f}")
+
+
+@pytest.mark.parametrize("B", [8, 16])
+def test_tiny_batched_decode_fin_path_vs_oracle(tiny, golden, B):
+    """Batched decode (5..16 rows) with in-kernel split-K finalisation: merge kernel + o_proj / down_proj
+    F32_FIN (residual, x' and per-tile-pair sums of squares) feeding PRO_X_RSTD GEMVs with two 16-row tiles
+    per workgroup.  Per-step logits of every row against the oracle, and against the unfused layer."""
+    from oracle import paligemma_oracle as O
+    eng, orc = tiny
+    g = golden("tiny")
+    ids_np = g["b1_input_ids"]
+    steps = 10
+    ref_ids, ref_logits = O.generate(orc, ids_np, g["b1_pixel_values"], np.ones_like(ids_np), steps,
+                                     stop_token=None, record_logits=True)
+    ids = torch.from_numpy(ids_np).cuda().repeat(B, 1)
+    px = torch.from_numpy(g["b1_pixel_values"]).cuda().repeat(B, 1, 1, 1)
+    outs = {}
+    for use_fin in (True, False):
+        eng.USE_FIN = use_fin
+        try:
+            cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), steps)
+            st = eng.decode_state(B, cache, nxt, steps)
+            lgs = []
+            for t in range(1, steps):
+                st["ids"].fill_(ref_ids[t - 1])
+                lg = eng.decode_step(st, cache, feats, dict(do_sample=False)).clone()
+                for row in (0, B - 1):
+                    assert err(lg[row:row + 1].cpu().numpy(), ref_logits[t]) < TOL, (use_fin, t, row)
+                lgs.append(lg)
+            outs[use_fin] = torch.stack(lgs)
+        finally:
+            eng.USE_FIN = type(eng).USE_FIN
+    assert err(outs[True].cpu().numpy(), outs[False].cpu().numpy()) < 5e-3
