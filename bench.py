@@ -290,6 +290,7 @@ def main():
     traffic, traffic_src = pmc_traffic()
     kern_desc = f"gemv_kernel<GELU_MUL,2> (decode gate/up, 2x{eng.w.inter}x{eng.w.hidden} bf16)"
 
+    comm_used = eng.comm
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del state, eng
@@ -332,8 +333,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(rec), flush=True)
-    if hasattr(eng.comm, "check"):
-        eng.comm.check()                       # a timed-out exchange invalidates the run
+    if hasattr(comm_used, "check"):
+        comm_used.check()                      # a timed-out exchange invalidates the run
     if dist is not None:
         dist.destroy_process_group()
 
