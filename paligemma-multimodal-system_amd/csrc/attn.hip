@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
 // skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
 // V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row);
 // K dims past D (D < DP) are never read from memory.
-template <int DP, int DT, int WAVES>
+template <int DP, int DT, int WAVES, int RPW>
 __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   constexpr int KS = DP / 32;
   constexpr int NCH = DP / 8;                      // 16-B chunks per K row
@@ -377,18 +377,21 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   const int Lkv = a.Lkv;
   const int R = a.Lq * a.G;
   const int D = a.D;
-  const int r = (blockIdx.x * WAVES + wave) * 16 + c;
-  const bool rvalid = r < R;
-  const int pos = rvalid ? r / a.G : 0;
-  const int hq = kvh * a.G + (rvalid ? r % a.G : 0);
-
-  bf16x8 qf[KS];
-  {
-    const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * D;
+  // RPW groups of 16 query rows per wave: every K / V^T fragment read from LDS feeds RPW MFMAs
+  int pos[RPW], hq[RPW];
+  bool rvalid[RPW];
+  bf16x8 qf[RPW][KS];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    const int r = ((blockIdx.x * WAVES + wave) * RPW + i) * 16 + c;
+    rvalid[i] = r < R;
+    pos[i] = rvalid[i] ? r / a.G : 0;
+    hq[i] = kvh * a.G + (rvalid[i] ? r % a.G : 0);
+    const bf16_t* qp = a.q + ((long)b * a.Lq + pos[i]) * a.q_rs + (long)hq[i] * D;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int d0 = 32 * s + 8 * g;
-      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
+      qf[i][s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid[i] && d0 < D));
     }
   }
   const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
@@ -414,10 +417,15 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     }
   };
 
-  f32x4 o[DT];
+  f32x4 o[RPW][DT];
+  float m[RPW], l[RPW];
 #pragma unroll
-  for (int tt = 0; tt < DT; ++tt) o[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
+  for (int i = 0; i < RPW; ++i) {
+    m[i] = -INFINITY;
+    l[i] = 0.f;
+#pragma unroll
+    for (int tt = 0; tt < DT; ++tt) o[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int nblk = (Lkv + 63) / 64;
 
   stage(0, 0);
@@ -429,56 +437,67 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     const char* kimg = smem + (ib & 1) * STAGE;
     const char* vimg = kimg + KIMG;
     // ---- S^T for 4 groups of 16 keys
-    f32x4 sc[4];
+    f32x4 sc[RPW][4];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) sc[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < RPW; ++i)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) sc[i][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         const bf16x8 kf = *(const bf16x8*)(kimg + ((kt * NCH + 4 * s + g) * 16 + c) * 16);
-        sc[kt] = mfma16(kf, qf[s], sc[kt]);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) sc[i][kt] = mfma16(kf, qf[i][s], sc[i][kt]);
       }
-    // lane holds S[key = kb + 16 kt + 4g + j][q = c]
-    float x[16];
+    // lane holds S[key = kb + 16 kt + 4g + j][q = c] of each row group
+    bf16x8 pf[RPW][2];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[kt][j] * a.scale_log2;
-    if (kb + 64 > Lkv) {
+    for (int i = 0; i < RPW; ++i) {
+      float x[16];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (kb + 16 * kt + 4 * g + j >= Lkv) x[4 * kt + j] = -INFINITY;
+        for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[i][kt][j] * a.scale_log2;
+      if (kb + 64 > Lkv) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (kb + 16 * kt + 4 * g + j >= Lkv) x[4 * kt + j] = -INFINITY;
+      }
+      float bm = x[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) bm = fmaxf(bm, x[j]);
+      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      const float mn = fmaxf(m[i], bm);
+      const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+      float rs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[i] = l[i] * alpha + rs;
+      m[i] = mn;
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O
+#pragma unroll
+        for (int tt = 0; tt < DT; ++tt) o[i][tt] *= alpha;
+      }
+      // P^T operand of the two 32-key steps; slot 8g+j <-> key 32h + 4g + j (j < 4), 32h + 16 + 4g + j - 4
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        u32x4 pw;
+        pw[0] = pack_bf2(x[8 * h + 0], x[8 * h + 1]);
+        pw[1] = pack_bf2(x[8 * h + 2], x[8 * h + 3]);
+        pw[2] = pack_bf2(x[8 * h + 4], x[8 * h + 5]);
+        pw[3] = pack_bf2(x[8 * h + 6], x[8 * h + 7]);
+        pf[i][h] = __builtin_bit_cast(bf16x8, pw);
+      }
     }
-    float bm = x[0];
-#pragma unroll
-    for (int j = 1; j < 16; ++j) bm = fmaxf(bm, x[j]);
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-    const float mn = fmaxf(m, bm);
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);
-    float rs = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
-    m = mn;
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O
-#pragma unroll
-      for (int tt = 0; tt < DT; ++tt) o[tt] *= alpha;
-    }
-    // ---- O^T += V^T . P^T over two 32-key steps; slot 8g+j <-> key 32h + 4g + j (j < 4), 32h + 16 + 4g + j - 4
+    // ---- O^T += V^T . P^T: one V^T fragment read feeds the RPW row groups
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      u32x4 pw;
-      pw[0] = pack_bf2(x[8 * h + 0], x[8 * h + 1]);
-      pw[1] = pack_bf2(x[8 * h + 2], x[8 * h + 3]);
-      pw[2] = pack_bf2(x[8 * h + 4], x[8 * h + 5]);
-      pw[3] = pack_bf2(x[8 * h + 6], x[8 * h + 7]);
-      const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
 #pragma unroll
       for (int tt = 0; tt < DT; ++tt) {
         const int row = 16 * tt + c;
@@ -487,23 +506,28 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
         const int c0 = 4 * h, c1 = 4 * h + 2;                 // 16-B chunks of keys 32h + 4g.. and 32h + 16 + 4g..
         const u32x2 v0 = *(const u32x2*)(vr + ((c0 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
         const u32x2 v1 = *(const u32x2*)(vr + ((c1 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
-        o[tt] = mfma16(__builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]}), pf, o[tt]);
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]});
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) o[i][tt] = mfma16(vf, pf[i][h], o[i][tt]);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next block landed (this wave's loads)
     __builtin_amdgcn_s_barrier();                        // ... every wave's; this buffer fully read
   }
-  if (!rvalid) return;
-  const float inv = 1.0f / l;
-  bf16_t* op = a.o + ((long)b * a.Lq + pos) * a.o_rs + (long)hq * D;
 #pragma unroll
-  for (int tt = 0; tt < DT; ++tt) {
-    const int d = 16 * tt + 4 * g;
-    if (d < D) {
-      u32x2 p;
-      p[0] = pack_bf2(o[tt][0] * inv, o[tt][1] * inv);
-      p[1] = pack_bf2(o[tt][2] * inv, o[tt][3] * inv);
-      *(u32x2*)(op + d) = p;
+  for (int i = 0; i < RPW; ++i) {
+    if (!rvalid[i]) continue;
+    const float inv = 1.0f / l[i];
+    bf16_t* op = a.o + ((long)b * a.Lq + pos[i]) * a.o_rs + (long)hq[i] * D;
+#pragma unroll
+    for (int tt = 0; tt < DT; ++tt) {
+      const int d = 16 * tt + 4 * g;
+      if (d < D) {
+        u32x2 p;
+        p[0] = pack_bf2(o[i][tt][0] * inv, o[i][tt][1] * inv);
+        p[1] = pack_bf2(o[i][tt][2] * inv, o[i][tt][3] * inv);
+        *(u32x2*)(op + d) = p;
+      }
     }
   }
 }
@@ -564,12 +588,37 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   }
 }
 
+// Flash attention, 16-row query groups per wave.  2 (one K / V^T fragment read feeding two row groups,
+// 4 waves at head_dim 256) measured 0.81x at pt-448 Gemma, 0.95x / 1.03x at SigLIP 448 / 896: default 1.
+#ifndef PG_FA_RPW
+#define PG_FA_RPW 1
+#endif
+
+template <int DP, int DT>
+static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const AttnArgs& a) {
+  if constexpr (PG_FA_RPW == 2) {
+    if constexpr (DP <= 96) {       // (DP 128 at 8 x 32 rows needs > 256 registers: 1 wave / SIMD)
+      if (waves == 8 && rpw == 2) {
+        hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 2>), grid, dim3(512), 0, stream, a);
+        return;
+      }
+    }
+    if (waves == 4 && rpw == 2) {
+      hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 4, 2>), grid, dim3(256), 0, stream, a);
+      return;
+    }
+  }
+  if (waves == 8)
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 1>), grid, dim3(512), 0, stream, a);
+  else
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 4, 1>), grid, dim3(256), 0, stream, a);
+}
+
+
 #define ATTN_DISPATCH(DP_, DT_)                                                             \
   if (DP == DP_ && DT == DT_) {                                                              \
-    if (fa_waves == 8)                                                                       \
-      hipLaunchKernelGGL((attn_fa_kernel<DP_, DT_, 8>), grid, dim3(512), 0, stream, a);      \
-    else if (fa_waves == 4)                                                                  \
-      hipLaunchKernelGGL((attn_fa_kernel<DP_, DT_, 4>), grid, dim3(256), 0, stream, a);      \
+    if (fa_waves)                                                                            \
+      launch_fa<DP_, DT_>(fa_waves, fa_rpw, grid, stream, a);                                \
     else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
     else                                                                                     \
@@ -604,11 +653,22 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
                        k_hs % 8 == 0 && q_rs % 8 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 &&
                        ((uintptr_t)vt & 15) == 0;
   // LDS-DMA flash kernel for every unmasked prefill; 8 waves (128 rows) per workgroup once that fills the chip
-  int fa_waves = 0;
+  int fa_waves = 0, fa_rpw = 1;
   if (split_keys == 0 && mask == nullptr && aligned && lkv_dev == nullptr && PG_ATTN_FA) {
-    const long wg128 = (long)((Lq * G + 127) / 128) * Hkv * B;
-    fa_waves = wg128 >= 256 ? 8 : 4;
-    grid = dim3((Lq * G + 16 * fa_waves - 1) / (16 * fa_waves), Hkv, B);
+    auto wgs = [&](int rows) { return (long)((Lq * G + rows - 1) / rows) * Hkv * B; };
+    // two 16-row groups per wave (half the LDS fragment reads per flop) when the grid still fills the chip:
+    // 8 waves x 32 rows for head_dim <= 96, else 4 waves x 32 rows (their accumulators need 1 wave / SIMD)
+    if (PG_FA_RPW == 2 && DP <= 96 && wgs(256) >= 256) {
+      fa_waves = 8;
+      fa_rpw = 2;
+    } else if (PG_FA_RPW == 2 && wgs(128) >= 256) {
+      fa_waves = 4;
+      fa_rpw = 2;
+    } else {
+      fa_waves = wgs(128) >= 256 ? 8 : 4;
+    }
+    const int rows = 16 * fa_waves * fa_rpw;
+    grid = dim3((Lq * G + rows - 1) / rows, Hkv, B);
   }
   const bool use_lds = fa_waves == 0 && split_keys == 0 && wgs16 >= 1024 && aligned;
   if (fa_waves) {

@@ -14,6 +14,8 @@ SHAPES = {  # name: (B, L, Hq, Hkv, D)
     "siglip448x16": (16, 1024, 16, 16, 72),
     "gemma224": (1, 264, 8, 1, 256),
     "siglip224": (1, 256, 16, 16, 72),
+    "gemma896x32": (32, 4104, 8, 1, 256),
+    "siglip896x32": (32, 4096, 16, 16, 72),
 }
 only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else list(SHAPES)
 reps = int(os.environ.get("REPS", "10"))
