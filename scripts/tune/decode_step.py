@@ -21,6 +21,7 @@ ap.add_argument("--split-down", type=int, default=None)
 ap.add_argument("--split-keys", type=int, default=None)
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--split-target", type=int, default=None)
+ap.add_argument("--fp8", action="store_true")
 ap.add_argument("--no-fuse-ao", action="store_true", help="attention as its own kernel (not inside o_proj)")
 a = ap.parse_args()
 
@@ -29,7 +30,7 @@ import bench  # noqa: E402
 
 cfg = configs.CONFIGS[a.config]
 sd = synthetic.SyntheticStateDict(cfg)
-eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=a.fp8))
 if a.split_o:
     eng.split_o = a.split_o
 if a.split_down:
