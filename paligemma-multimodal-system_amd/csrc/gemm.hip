@@ -22,6 +22,9 @@
 
 #include "attn_common.h"
 
+#ifndef PG_G256_STAGGER
+#define PG_G256_STAGGER 1       // gemm256: wave groups one barrier apart (MFMA of one || LDS reads of the other); +4-14%
+#endif
 #ifndef PG_G256_PREFETCH
 #define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
 #endif
@@ -531,6 +534,47 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   }
   __builtin_amdgcn_s_barrier();
 
+  if constexpr (PG_G256_STAGGER && !F8) {
+    // Wave groups wr = 0 / 1 (one wave of each per SIMD) run one barrier apart, two barriers per phase:
+    // while one group issues its phase's LDS reads and DMA, the other runs its MFMAs.  With the offset, a
+    // group's reads must be complete before its phase's first barrier (lgkmcnt(0) there: the other group
+    // restages right after it) and the tile's vmcnt wait sits before phase 3's first barrier (the other
+    // group reads the retired halves one barrier earlier than this one) -- guide: "one barrier MORE when
+    // two wave groups run staggered".
+    auto bar = [] { __builtin_amdgcn_s_barrier(); };
+    auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    if (wr == 1) bar();
+    for (int t = 0; t < nk; ++t) {
+      const char* buf = smem + (t & 1) * 4 * HALF;
+      read_a(buf, fa0);
+      read_b(buf + 2 * HALF, fb0);
+      if (t + 1 < nk) stage(2, t + 1);
+      lgkm0();
+      bar();
+      mma(0, 0, fa0, fb0);
+      bar();
+      read_b(buf + 3 * HALF, fb0);
+      if (t + 2 < nk) stage(0, t + 2);
+      lgkm0();
+      bar();
+      mma(0, 1, fa0, fb0);
+      bar();
+      read_a(buf + 1 * HALF, fa0);
+      if (t + 2 < nk) stage(3, t + 2);
+      lgkm0();
+      bar();
+      mma(1, 1, fa0, fb0);
+      bar();
+      read_b(buf + 2 * HALF, fb0);
+      if (t + 2 < nk) stage(1, t + 2);
+      if (t + 2 < nk) wait_vm(6); else wait_vm(0);
+      lgkm0();
+      bar();
+      mma(1, 0, fa0, fb0);
+      bar();
+    }
+    if (wr == 0) bar();     // same barrier count for both groups
+  } else
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * 4 * HALF;
     if constexpr (PG_G256_PREFETCH && !F8) {   // (fp8: the early reads would spill)
