@@ -224,13 +224,15 @@ __global__ __launch_bounds__(256) void argmax_partial_kernel(const float* __rest
 
 // final pass; also advances the decode state when asked:
 //   out_ids[b] = argmax ; hist[(*step) * B + b] = argmax ; pos[b] += 1 ; (*kv_len) += 1 ; (*step) += 1
-__global__ __launch_bounds__(64) void argmax_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                          int B, int64_t* __restrict__ out_ids, int64_t* __restrict__ hist,
-                                                          int hist_rows, int* __restrict__ step, int* __restrict__ pos,
-                                                          int* __restrict__ kv_len) {
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(1024) void argmax_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                            int B, int64_t* __restrict__ out_ids, int64_t* __restrict__ hist,
+                                                            int hist_rows, int* __restrict__ step, int* __restrict__ pos,
+                                                            int* __restrict__ kv_len) {
+  // one wave per row (rows strided over the block's waves): the rows' chunk winners load in parallel
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int st = step ? *step : 0;
-  for (int b = 0; b < B; ++b) {
+  __syncthreads();                             // every wave has read *step before thread 0 advances it
+  for (int b = wave; b < B; b += nw) {
     float bv = pv[b * AM_CHUNKS + lane];
     int bi = pi[b * AM_CHUNKS + lane];
 #pragma unroll
@@ -245,18 +247,20 @@ __global__ __launch_bounds__(64) void argmax_final_kernel(const float* __restric
       if (pos) pos[b] += 1;
     }
   }
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     if (kv_len) *kv_len += 1;
     if (step) *step = st + 1;
   }
 }
 
+static inline int am_waves(int B) { return B < 1 ? 1 : (B > 16 ? 16 : B); }
+
 // vocabulary-parallel greedy (tensor parallelism): the local (max, first index + vocab_offset) per row,
 // as float pairs [B][2] to be all-gathered; then pg_argmax_merge picks the global winner.
-__global__ __launch_bounds__(64) void argmax_pairs_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
-                                                          int B, int vocab_offset, float* __restrict__ pairs) {
-  const int lane = threadIdx.x;
-  for (int b = 0; b < B; ++b) {
+__global__ __launch_bounds__(1024) void argmax_pairs_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                            int B, int vocab_offset, float* __restrict__ pairs) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int b = wave; b < B; b += nw) {
     float bv = pv[b * AM_CHUNKS + lane];
     int bi = pi[b * AM_CHUNKS + lane];
 #pragma unroll
@@ -293,7 +297,7 @@ extern "C" int pg_argmax_pairs(const float* logits, long ld, int B, int V, int v
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
-  hipLaunchKernelGGL(argmax_pairs_kernel, dim3(1), dim3(64), 0, stream, pv, pi, B, vocab_offset, pairs);
+  hipLaunchKernelGGL(argmax_pairs_kernel, dim3(1), dim3(64 * am_waves(B)), 0, stream, pv, pi, B, vocab_offset, pairs);
   PG_LAUNCH_CHECK();
   return 0;
 }
@@ -314,7 +318,7 @@ extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* works
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
-  hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(64), 0, stream, pv, pi, B, out_ids, hist, hist_rows, step, pos,
+  hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(64 * am_waves(B)), 0, stream, pv, pi, B, out_ids, hist, hist_rows, step, pos,
                      kv_len);
   PG_LAUNCH_CHECK();
   return 0;

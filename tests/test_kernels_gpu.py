@@ -283,6 +283,23 @@ def test_argmax_first_index_and_state_advance():
     step.fill_(4)
     ops.argmax(x, ids, ws, hist=guard[:4], step=step, pos=pos, kv_len=kv)
     assert (guard[4:] == -7).all() and step.item() == 5 and ids.cpu().tolist() == want.tolist()
+    # more rows than the final pass has waves (16): rows strided over the waves, ties across chunk edges
+    B = 20
+    x = torch.randn(B, V).cuda()
+    x[:, 4019] = 40.0
+    x[:, 4020] = 40.0
+    x[7, 257215] = 60.0
+    ids = torch.empty(B, dtype=torch.int64, device="cuda")
+    ws = torch.empty(B * 64 * 2, device="cuda")
+    hist = torch.zeros(3, B, dtype=torch.int64, device="cuda")
+    step = torch.tensor([1], dtype=torch.int32, device="cuda")
+    pos = torch.arange(B, dtype=torch.int32, device="cuda")
+    kv.fill_(3)
+    ops.argmax(x, ids, ws, hist=hist, step=step, pos=pos, kv_len=kv)
+    want = torch.argmax(x.cpu(), -1)
+    assert ids.cpu().tolist() == want.tolist() and ids[7].item() == 257215 and ids[0].item() == 4019
+    assert hist[1].cpu().tolist() == want.tolist() and (hist[0] == 0).all() and (hist[2] == 0).all()
+    assert step.item() == 2 and kv.item() == 4 and pos.cpu().tolist() == list(range(1, B + 1))
 
 
 def test_topp_matches_reference_filter(golden):
