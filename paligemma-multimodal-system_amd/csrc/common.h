@@ -24,10 +24,11 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
-  // torch gelu(approximate="tanh"): 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3)))
-  const float k = 0.7978845608028654f;
-  float u = k * (x + 0.044715f * x * x * x);
-  return 0.5f * x * (1.0f + tanhf(u));
+  // torch gelu(approximate="tanh"): 0.5 x (1 + tanh(u)), u = sqrt(2/pi) (x + 0.044715 x^3), evaluated as
+  // x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32 (~1 ulp each) instead of
+  // libm tanhf, exact limits at both tails (x -> 0 for u -> -inf, x for u -> +inf)
+  const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.8853900817779268f * u));
 }
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {

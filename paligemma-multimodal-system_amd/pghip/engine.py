@@ -28,6 +28,7 @@ per-rank (max, index) pairs, and full logits are assembled by a zero-padded all-
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -65,6 +66,8 @@ class PaliGemmaEngine:
     DECODE_SPLIT_O = 2      # split-K of o_proj at decode (partials reduced by the next RMSNorm)
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
+    # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
+    PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
@@ -244,9 +247,12 @@ class PaliGemmaEngine:
             xs = self._buf(f"xs_{K}", (M,), torch.float32)
             ops.quant_fp8(x, x8, xs, M=M)
             return ops.gemm8(x8, xs, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa)
+        W, flag = Lw[name + "_w"], w.wflag
+        if M >= self.PREFILL_ROWMAJOR_MIN_M and name + "_wr" in Lw:
+            W, flag = Lw[name + "_wr"], 0
         if fa is not None:
-            return ops.gemm_fused(x, Lw[name + "_w"], out, fa, epi=epi | w.wflag, M=M)
-        return ops.gemm(x, Lw[name + "_w"], out, epi=epi | w.wflag, ksplit=ksplit)
+            return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)
+        return ops.gemm(x, W, out, epi=epi | flag, ksplit=ksplit)
 
     def _norm(self, resid: torch.Tensor, norm_w: torch.Tensor, part, nsplit: int, xn: torch.Tensor, M: int):
         """Gemma RMSNorm of the residual (+ split-K partials) feeding a linear: bf16 rows, or fp8 rows with

@@ -75,12 +75,13 @@ def quant_rows_fp8(w: torch.Tensor):
 
 class PackedWeights:
     def __init__(self, cfg: dict, get, device="cuda", parts=("vision", "proj", "text"), tp_rank: int = 0,
-                 tp_world: int = 1, fp8: bool = False):
+                 tp_world: int = 1, fp8: bool = False, prefill_rowmajor: bool = True):
         """fp8: also hold the Gemma decoder linears as fp8 e4m3 with per-output-channel scales (`<name>8`,
         `<name>_s8` in each layer dict) for the PG_FP8 GEMMs of prefill and batch > 16 decode (BASELINE
         configs[4]); the bf16 copies stay for the weight-streaming GEMV path (batch <= 16 decode)."""
         self.cfg = cfg
         self.fp8 = bool(fp8)
+        self.prefill_rowmajor = bool(prefill_rowmajor)   # keep row-major Gemma linears beside the packed ones
         self.tp_rank, self.tp_world = int(tp_rank), int(tp_world)
         if not 0 <= self.tp_rank < self.tp_world:
             raise ValueError(f"tp_rank {tp_rank} outside tp_world {tp_world}")
@@ -216,6 +217,11 @@ class PackedWeights:
             layer = dict(
                 in_w=f32(get(lp + "input_layernorm.weight")), qkv_w=pk(qkv_w), o_w=pk(o_w),
                 post_w=f32(get(lp + "post_attention_layernorm.weight")), gu_w=pk(gu), down_w=pk(down))
+            if self.frag and self.prefill_rowmajor and not self.fp8:
+                # row-major copies for the large-M prefill GEMMs: gemm256's LDS-DMA tile loads run 7-11%
+                # faster on them than on the fragment-packed image (scripts/tune/gemm_bench.py), and
+                # 3.96 GB more of the 288 GB HBM is cheap
+                layer.update(qkv_wr=qkv_w, o_wr=o_w, gu_wr=gu, down_wr=down)
             if self.fp8:
                 if H % 128 or (self.heads * hd) % 128:
                     raise ValueError("fp8 weights need hidden and heads*head_dim multiples of 128")
