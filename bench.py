@@ -147,6 +147,8 @@ def main():
                     help="Gemma linears as fp8 e4m3 (per-channel / per-row scales) for GEMMs over 16 rows, as BASELINE "
                     "configs[4]")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph-prefill", action="store_true",
+                    help="replay the prefill as one hipGraph (measured 0.96-0.97x of eager launches: off by default)")
     ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
                     "instead of greedy, as BASELINE configs[3]")
     args = ap.parse_args()
@@ -219,24 +221,43 @@ def main():
         graph_mode = "hipgraph"
     graph_cache = state["cache"]
 
-    def request():
-        # prefill into the graph's static cache / state, then replay the captured decode step
+    rows = eng._buf("p_rows", (B,), torch.int32)
+    rows.copy_(torch.arange(B, dtype=torch.int32) * L + (L - 1))
+    pos_pf = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
+
+    def prefill():
+        # vision + merge + Gemma prefill into the decode graph's static cache / state, first token sampled
         feats = eng.vision(px)
         resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
         eng.embed_merge(ids, feats, resid)
-        pos = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
-        rows = eng._buf("p_rows", (B,), torch.int32)
-        logits, _ = eng.gemma_prefill(resid, pos, graph_cache, B, L, logits_rows=rows)
+        logits, _ = eng.gemma_prefill(resid, pos_pf, graph_cache, B, L, logits_rows=rows)
         state["st"]["pos"].fill_(L + 1)
         state["st"]["kv_len"].fill_(L)
         state["st"]["step"].zero_()
         state["feats"].copy_(feats)
         eng.sample(logits, state["st"], sampler, advance=False)
+
+    # optionally the prefill's ~400 launches as one hipGraph (fixed request shape, as a serving replica would
+    # hold one per shape bucket); measured slower than eager launches on MI355X (pt-224 6.0 vs 5.76 ms,
+    # pt-448 x16 91.6 vs 89.0 ms), so eager is the default
+    prefill_run, prefill_mode = prefill, "eager"
+    if graph_mode == "hipgraph" and args.graph_prefill:
+        try:
+            prefill()                                  # every workspace allocated outside capture
+            torch.cuda.synchronize()
+            g_pf = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_pf):
+                prefill()
+            torch.cuda.synchronize()
+            prefill_run, prefill_mode = g_pf.replay, "hipgraph"
+        except Exception as e:
+            log(f"[bench] rank {rank}: prefill capture failed ({e}); eager prefill")
+            torch.cuda.synchronize()
+
+    def request():
+        prefill_run()
         for _ in range(T - 1):
             replay()
-
-    rows = eng._buf("p_rows", (B,), torch.int32)
-    rows.copy_(torch.arange(B, dtype=torch.int32) * L + (L - 1))
 
     def barrier():
         torch.cuda.synchronize()
@@ -264,11 +285,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     ev[0].record()
     for _ in range(3):
-        feats = eng.vision(px)
-        resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
-        eng.embed_merge(ids, feats, resid)
-        pos = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
-        eng.gemma_prefill(resid, pos, graph_cache, B, L, logits_rows=rows)
+        prefill_run()
     ev[1].record()
     state["st"]["kv_len"].fill_(L)
     state["st"]["pos"].fill_(L + 1)
@@ -317,7 +334,7 @@ def main():
             "config": {"workload": f"PaliGemma-3B-{args.config} image->text, batch {B}, prefill L={L}, "
                                    f"{T} {'top-p' if args.sample else 'greedy'} tokens ({baseline_ref})",
                        "global_batch": B * (world // tp), "seq_len": L + T,
-                       "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}-{args.comm}", "decode": graph_mode},
+                       "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}-{args.comm}", "decode": graph_mode, "prefill": prefill_mode},
             "prefill_ms": round(prefill_ms, 3),
             "prefill_tflops": round(pf_flops / (prefill_ms / 1e3) / 1e12, 2),
             "prefill_mfma_frac": round(pf_flops / (prefill_ms / 1e3) / 1e12 / BF16_PEAK_TFS, 4),
