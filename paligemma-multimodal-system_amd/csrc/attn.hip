@@ -22,6 +22,9 @@
 #ifndef PG_ATTN_FA
 #define PG_ATTN_FA 1      // prefill: the LDS-DMA flash kernel (0: the register-staged kernels)
 #endif
+#ifndef PG_FA_W12
+#define PG_FA_W12 1       // prefill, head_dim 256: 12-wave workgroups when they fill the one-per-CU rounds better
+#endif
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
@@ -608,6 +611,12 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
       return;
     }
   }
+  if constexpr (DP == 256) {
+    if (waves == 12) {
+      hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 12, 1>), grid, dim3(768), 0, stream, a);
+      return;
+    }
+  }
   if (waves == 8)
     hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 1>), grid, dim3(512), 0, stream, a);
   else
@@ -666,6 +675,9 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
       fa_rpw = 2;
     } else {
       fa_waves = wgs(128) >= 256 ? 8 : 4;
+      // head_dim 256 (166 VGPRs, fits 3 waves / SIMD): 12 waves when the one-workgroup-per-CU rounds cost
+      // less in total (pt-448 x16 Gemma: 688 workgroups in 3 rounds of 192 rows vs 1040 in 5 rounds of 128)
+      if (PG_FA_W12 && DP == 256 && fa_waves == 8 && ((wgs(192) + 255) / 256) * 12 < ((wgs(128) + 255) / 256) * 8) fa_waves = 12;
     }
     const int rows = 16 * fa_waves * fa_rpw;
     grid = dim3((Lq * G + rows - 1) / rows, Hkv, B);

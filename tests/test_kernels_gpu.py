@@ -171,7 +171,8 @@ def test_attention_vision_layout(B, N, nh, hd):
 
 @pytest.mark.parametrize("B,L,nh,nkv,hd,masked", [(1, 264, 8, 1, 256, False), (2, 24, 4, 1, 32, True),
                                                   (1, 70, 8, 2, 64, False),
-                                                  (8, 300, 8, 1, 256, False), (16, 130, 8, 1, 256, True)])
+                                                  (8, 300, 8, 1, 256, False), (16, 130, 8, 1, 256, True),
+                                                  (14, 300, 8, 1, 256, False)])   # 12-wave flash kernel
 def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode."""
     from pghip import ops
