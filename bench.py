@@ -40,6 +40,7 @@ except Exception:  # pragma: no cover
     BASELINE_METRIC = "image->text tokens/sec + prefill ms, PaliGemma-3B-224 at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFS = 2500.0     # dense bf16 MFMA
+FP8_PEAK_TFS = 5000.0      # dense fp8 e4m3 MFMA
 
 
 def log(*a):
@@ -69,6 +70,14 @@ def prefill_flops(cfg, B, L):
     per = 2 * L * H * (nh * hd + 2 * nkv * hd) + 2 * L * nh * hd * H + 2 * L * H * I * 3 + 4 * L * L * nh * hd
     txt = t["num_hidden_layers"] * per + 2 * H * t["vocab_size"]
     return B * (vis + txt)
+
+
+def gemma_linear_flops(cfg, B, L):
+    """The Gemma decoder linears' share of prefill_flops (the part the --fp8 path runs on e4m3 MFMA)."""
+    t = cfg["text_config"]
+    H, I, nh, nkv, hd = t["hidden_size"], t["intermediate_size"], t["num_attention_heads"], t["num_key_value_heads"], 256
+    per = 2 * L * H * (nh * hd + 2 * nkv * hd) + 2 * L * nh * hd * H + 2 * L * H * I * 3
+    return B * t["num_hidden_layers"] * per
 
 
 def time_dominant_kernel(eng, reps=50):
@@ -301,6 +310,9 @@ def main():
     kv_bytes = B * (L + T // 2) * eng.w.t_layers * 2 * eng.w.kv_heads * eng.w.head_dim * 2
     decode_hbm = (step_bytes + kv_bytes) / (decode_ms_tok / 1e3) / 1e9
     pf_flops = prefill_flops(cfg, B, L)
+    # roofline time of the prefill: fp8 flops (Gemma linears under --fp8) at the dense fp8 peak, the rest at bf16
+    f8 = gemma_linear_flops(cfg, B, L) if args.fp8 and B * L > 16 else 0
+    pf_ideal_s = (pf_flops - f8) / (BF16_PEAK_TFS * 1e12) + f8 / (FP8_PEAK_TFS * 1e12)
 
     kern_s, kern_bytes = time_dominant_kernel(eng)
     achieved = kern_bytes / kern_s / 1e9
@@ -337,7 +349,7 @@ def main():
                        "parallelism": f"dp{world}" if tp == 1 else f"tp{tp}-{args.comm}", "decode": graph_mode, "prefill": prefill_mode},
             "prefill_ms": round(prefill_ms, 3),
             "prefill_tflops": round(pf_flops / (prefill_ms / 1e3) / 1e12, 2),
-            "prefill_mfma_frac": round(pf_flops / (prefill_ms / 1e3) / 1e12 / BF16_PEAK_TFS, 4),
+            "prefill_mfma_frac": round(pf_ideal_s / (prefill_ms / 1e3), 4),
             "decode_ms_per_token": round(decode_ms_tok, 4),
             "decode_tok_s": round(B / (decode_ms_tok / 1e3), 1),
             "decode_hbm_gbs": round(decode_hbm, 1),

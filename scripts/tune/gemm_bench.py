@@ -28,7 +28,10 @@ SHAPES = [  # name, M, N, K, epi, frag
     ("sq8192", 8192, 8192, 8192, ops.EPI_BF16, False),
 ]
 res = {}
+only = sys.argv[sys.argv.index("--only") + 1].split(",") if "--only" in sys.argv else None
 for name, M, N, K, epi, frag in SHAPES:
+    if only and name not in only:
+        continue
     A = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     W = ((torch.rand(N, K, device="cuda") * 2 - 1) / K ** 0.5).to(torch.bfloat16)
     if frag:
