@@ -692,6 +692,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_T_NOFIN
 #define PG_T_NOFIN 0
 #endif
+#ifndef PG_GEMV_QKV_NT1
+#define PG_GEMV_QKV_NT1 1   // batched (M > 4) q|k|v GEMV with one 16-row tile per workgroup
+#endif
 #ifndef PG_GEMV_D2
 #define PG_GEMV_D2 4
 #endif
@@ -989,13 +992,17 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
   // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
   // own row, so the row total is a reduction over the 4 lane groups
-  constexpr int SSL = (PRO == 4 && NT == 2) ? 16 : 4;
+  // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- run the DEPTH = PG_GEMV_D2 ring and use
+  // the same 16-entry layout as the two-tile form)
+  static_assert(PG_GEMV_D2 != 8, "the one-tile M > 4 GEMV is told apart from the M <= 4 one by its ring depth");
+  constexpr bool SS16 = PRO == 4 && (NT == 2 || DEPTH != 8);
+  constexpr int SSL = SS16 ? 16 : 4;
   float ssv[SSL];
 #pragma unroll
   for (int k = 0; k < SSL; ++k) ssv[k] = 0.f;
   if constexpr (PRO == 4) {
     if (wave == 0) {
-      if (NT == 2 && M > 2) {
+      if (SS16 && M > 2) {
         const int rr = min(r, M - 1);
 #pragma unroll
         for (int k = 0; k < SSL; ++k) {
@@ -1123,7 +1130,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < SSL; ++k) ss += ssv[k];
-    if (NT == 2 && M > 2) {
+    if (SS16 && M > 2) {
       ss += __shfl_xor(ss, 16, 64);
       ss += __shfl_xor(ss, 32, 64);
     } else {
@@ -1294,7 +1301,12 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
       lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
     }
   }
-  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
+  if (PG_GEMV_QKV_NT1 && EPI == PG_EPI_QKV_ROPE && e.M > 4) {
+    // batched q|k|v (2560 rows): one tile per workgroup doubles the grid to 160 workgroups
+    dim3 grid(ntiles, ksplit);
+    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
+                       e);
+  } else if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
     dim3 grid((ntiles + 1) / 2, ksplit);
     hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
                        e);
