@@ -77,6 +77,9 @@ typedef struct PgFusedArgs {
                                only the non-empty splits are merged                                            */
   const float* a_scale;     /* PG_FP8: [M] row scales of A (dequantised A = q * a_scale[m])                      */
   const float* w_scale;     /* PG_FP8: [N] row scales of W, in W's row order                                   */
+  int slab_rows;            /* PG_EPI_F32 split-K: rows between slabs (slab z of row m at C + (z*slab_rows + m)*ldc);
+                               0 = M.  Lets a GEMM be issued as row blocks that write into one [ksplit][rows][N]
+                               partial tensor (C pointing at the block's first row)                            */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,

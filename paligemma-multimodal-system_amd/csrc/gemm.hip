@@ -83,6 +83,7 @@ struct PgFusedArgs {
   // C[m][n] is multiplied by a_scale[m] * w_scale[n] before the epilogue
   const float* a_scale;      // [M]
   const float* w_scale;      // [N] (in W's row order, e.g. the packed q|k|v or interleaved gate/up rows)
+  int slab_rows;             // PG_EPI_F32 split-K: rows between slabs (0 = M); lets a GEMM run as row blocks
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -180,7 +181,8 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x
   if (m >= e.M || n0 >= e.N) return;
   if (e.bias && (EPI != PG_EPI_F32 || z == 0)) v += load4_guard(e.bias, n0, e.N);
   if constexpr (EPI == PG_EPI_F32) {
-    float* C = (float*)e.C + (size_t)z * e.M * e.ldc + (size_t)m * e.ldc;
+    const size_t srows = e.f.slab_rows > 0 ? (size_t)e.f.slab_rows : (size_t)e.M;
+    float* C = (float*)e.C + ((size_t)z * srows + m) * e.ldc;
     if (n0 + 3 < e.N) {
       *(f32x4*)(C + n0) = v;
     } else {
@@ -1301,12 +1303,16 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
       lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
     }
   }
-  if (PG_GEMV_QKV_NT1 && EPI == PG_EPI_QKV_ROPE && e.M > 4) {
-    // batched q|k|v (2560 rows): one tile per workgroup doubles the grid to 160 workgroups
-    dim3 grid(ntiles, ksplit);
-    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
-                       e);
-  } else if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
+  if constexpr (PG_GEMV_QKV_NT1 && EPI == PG_EPI_QKV_ROPE) {
+    if (e.M > 4) {
+      // batched q|k|v (2560 rows): one tile per workgroup doubles the grid to 160 workgroups
+      dim3 grid(ntiles, ksplit);
+      hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw,
+                         K, e);
+      return;
+    }
+  }
+  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
     dim3 grid((ntiles + 1) / 2, ksplit);
     hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
                        e);

@@ -25,7 +25,8 @@ class PgFusedArgs(C.Structure):
                 ("slot_base", C.c_int), ("kc", C.c_void_p), ("vtc", C.c_void_p), ("smax", C.c_int),
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
-                ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p)]
+                ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
+                ("slab_rows", C.c_int)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)

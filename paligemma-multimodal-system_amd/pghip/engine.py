@@ -68,6 +68,7 @@ class PaliGemmaEngine:
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
+    ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
@@ -250,9 +251,32 @@ class PaliGemmaEngine:
         W, flag = Lw[name + "_w"], w.wflag
         if M >= self.PREFILL_ROWMAJOR_MIN_M and name + "_wr" in Lw:
             W, flag = Lw[name + "_wr"], 0
+        if fa is None and epi == ops.EPI_F32 and self.ROW_BLOCKS:
+            Mh = self._row_head(M, W.shape[0], ksplit)
+            if Mh:
+                # the 256-row tiles of the first Mh rows fill whole rounds of CUs; the ragged last rows
+                # (pt-448 x16: 128 of 16512) run as a small GEMM instead of one more mostly idle round.
+                # Both write the same [ksplit][M][N] slabs (PgFusedArgs.slab_rows)
+                fr = ops.fused_args(slab_rows=M)
+                ops.gemm_fused(x[:Mh], W, out, fr, epi=epi | flag, M=Mh, ksplit=ksplit, ldc=out.stride(-2))
+                tail = out.view(-1)[Mh * out.stride(-2):]
+                return ops.gemm_fused(x[Mh:M], W, tail, fr, epi=epi | flag, M=M - Mh, ksplit=ksplit,
+                                      ldc=out.stride(-2))
         if fa is not None:
             return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)
         return ops.gemm(x, W, out, epi=epi | flag, ksplit=ksplit)
+
+    @staticmethod
+    def _row_head(M: int, N: int, ksplit: int, cus: int = ops.CUS) -> int:
+        """Rows of an fp32-slab prefill GEMM to issue as whole 256-row tiles, 0 to keep it one launch: only
+        in the one-tile-per-CU regime (>= `cus` 256x256 tiles) and when dropping the ragged last row tile
+        saves a round of CUs (Gemma o / down at pt-448 x16: 2.03 -> 2 and 6.1 -> 6 rounds)."""
+        Mh = M // 256 * 256
+        tn = (N + 255) // 256
+        if Mh == M or Mh == 0 or (M + 255) // 256 * tn * ksplit < cus:
+            return 0
+        rounds = lambda tiles: (tiles + cus - 1) // cus  # noqa: E731
+        return Mh if rounds(Mh // 256 * tn * ksplit) < rounds((M + 255) // 256 * tn * ksplit) else 0
 
     def _norm(self, resid: torch.Tensor, norm_w: torch.Tensor, part, nsplit: int, xn: torch.Tensor, M: int):
         """Gemma RMSNorm of the residual (+ split-K partials) feeding a linear: bf16 rows, or fp8 rows with

@@ -67,6 +67,25 @@ def test_gemm_split_k_partials(M):
         assert err(part.sum(0), A.float() @ W.float().t() + bias) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,s", [(300, 256, 512, 2), (16512, 2048, 2048, 1), (16512, 2048, 4096, 3)])
+def test_gemm_slab_rows_row_blocks(M, N, K, s):
+    """PgFusedArgs.slab_rows: a split-K fp32 GEMM issued as a head of whole 256-row tiles plus a ragged tail,
+    both writing into one [s][M][N] slab tensor (engine._row_head), equals the one-launch result."""
+    from pghip import ops
+    A, W = rnd(M, K, seed=31), rnd(N, K, scale=1 / math.sqrt(K), seed=32)
+    Mh = M // 256 * 256
+    one = torch.empty(s, M, N, dtype=torch.float32, device="cuda")
+    ops.gemm(A, W, one, epi=ops.EPI_F32, ksplit=s)
+    two = torch.full((s, M, N), float("nan"), dtype=torch.float32, device="cuda")
+    fr = ops.fused_args(slab_rows=M)
+    ops.gemm_fused(A[:Mh], W, two, fr, epi=ops.EPI_F32, M=Mh, ksplit=s, ldc=N)
+    ops.gemm_fused(A[Mh:], W, two.view(-1)[Mh * N:], fr, epi=ops.EPI_F32, M=M - Mh, ksplit=s, ldc=N)
+    assert not torch.isnan(two).any()
+    ref = A.float() @ W.float().t()
+    assert err(two.sum(0), ref) < 1e-5 and err(one.sum(0), ref) < 1e-5
+    assert torch.equal(two[:, :Mh], one[:, :Mh])        # the head's tiles are the same launches' tiles
+
+
 @pytest.mark.parametrize("M", [1, 16, 150])
 def test_gemm_gelu_and_gelu_mul(M):
     from pghip import ops
