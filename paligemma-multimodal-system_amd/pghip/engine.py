@@ -69,6 +69,9 @@ class PaliGemmaEngine:
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
     ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
+    # ragged-N SigLIP GEMMs as head + tail launches: measured neutral at pt-448 x16 and pt-896 x32 (the small-tile
+    # tail costs what the saved round gave back; scripts/tune/run_s4_p.sh), so off
+    COL_BLOCKS = os.environ.get("PG_COL_BLOCKS", "0") == "1"
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
@@ -148,11 +151,11 @@ class PaliGemmaEngine:
                      aux_n=2 * hv)
             ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
                           B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5))
-            ops.gemm(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
+            self._gemm_cols(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
             ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
                               nsplit=s_o, out=xn)
-            ops.gemm(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"])
-            ops.gemm(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
+            self._gemm_cols(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"])
+            self._gemm_cols(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
             ns = s_2
             if taps is not None:                                          # debug: residual after the layer
                 taps.append((resid + part[:ns].sum(0)).clone())
@@ -265,6 +268,26 @@ class PaliGemmaEngine:
         if fa is not None:
             return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)
         return ops.gemm(x, W, out, epi=epi | flag, ksplit=ksplit)
+
+    def _gemm_cols(self, A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int, bias=None, ksplit: int = 1):
+        """ops.gemm; or, when the last 256-column tile is ragged and dropping it saves a round of CUs, the whole
+        256-column tiles and the remaining columns as two GEMMs into the same output (column views: same ldc
+        and slab stride).  SigLIP o / fc1 / fc2 at pt-448 x16: 320 -> 256, 1088 -> 1024, 640 -> 512 tiles."""
+        Nh = self._col_head(A.shape[0], W.shape[0], ksplit) if self.COL_BLOCKS else 0
+        if not Nh:
+            return ops.gemm(A, W, out, epi=epi, bias=bias, ksplit=ksplit)
+        ops.gemm(A, W[:Nh], out[..., :Nh], epi=epi, bias=None if bias is None else bias[:Nh], ksplit=ksplit)
+        return ops.gemm(A, W[Nh:], out[..., Nh:], epi=epi, bias=None if bias is None else bias[Nh:], ksplit=ksplit)
+
+    @staticmethod
+    def _col_head(M: int, N: int, ksplit: int, cus: int = ops.CUS) -> int:
+        """Columns to issue as whole 256-column tiles (0: one launch), in the one-tile-per-CU regime."""
+        Nh = N // 256 * 256
+        tm = (M + 255) // 256
+        if Nh == N or Nh == 0 or tm * ((N + 255) // 256) * ksplit < cus:
+            return 0
+        rounds = lambda tiles: (tiles + cus - 1) // cus  # noqa: E731
+        return Nh if rounds(tm * (Nh // 256) * ksplit) < rounds(tm * ((N + 255) // 256) * ksplit) else 0
 
     @staticmethod
     def _row_head(M: int, N: int, ksplit: int, cus: int = ops.CUS) -> int:

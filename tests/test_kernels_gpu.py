@@ -86,6 +86,30 @@ def test_gemm_slab_rows_row_blocks(M, N, K, s):
     assert torch.equal(two[:, :Mh], one[:, :Mh])        # the head's tiles are the same launches' tiles
 
 
+@pytest.mark.parametrize("M,N,K,epi,s", [(300, 300, 128, "gelu", 1), (300, 300, 128, "f32", 2),
+                                         (16384, 1152, 1152, "f32", 1), (16384, 4304, 1152, "gelu", 1)])
+def test_gemm_column_blocks(M, N, K, epi, s):
+    """engine._gemm_cols: whole 256-column tiles + the ragged remaining columns as two GEMMs on column views
+    of one output (bias sliced, slabs keep their stride) equal the one-launch GEMM."""
+    from pghip import ops
+    A, W = rnd(M, K, seed=33), rnd(N, K, scale=1 / math.sqrt(K), seed=34)
+    bias = torch.randn(N).cuda() * 0.1
+    e = ops.EPI_BF16_GELU if epi == "gelu" else ops.EPI_F32
+    shape = (M, N) if epi == "gelu" else (s, M, N)
+    dt = torch.bfloat16 if epi == "gelu" else torch.float32
+    one = torch.empty(shape, dtype=dt, device="cuda")
+    two = torch.full(shape, float("nan"), dtype=dt, device="cuda")
+    ops.gemm(A, W, one, epi=e, bias=bias, ksplit=s)
+    Nh = N // 256 * 256
+    ops.gemm(A, W[:Nh], two[..., :Nh], epi=e, bias=bias[:Nh], ksplit=s)
+    ops.gemm(A, W[Nh:], two[..., Nh:], epi=e, bias=bias[Nh:], ksplit=s)
+    assert not torch.isnan(two.float()).any()
+    got = two.float() if epi == "gelu" else two.sum(0)
+    want = A.float() @ W.float().t() + bias
+    want = torch.nn.functional.gelu(want, approximate="tanh") if epi == "gelu" else want
+    assert err(got, want) < (1e-2 if epi == "gelu" else 1e-5)
+
+
 @pytest.mark.parametrize("M", [1, 16, 150])
 def test_gemm_gelu_and_gelu_mul(M):
     from pghip import ops
