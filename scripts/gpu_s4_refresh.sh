@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=s4r
+T=${1:-s4r}
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/$T.tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/$T.tests.log; [ $rc -eq 0 ] || exit 1
