@@ -1474,6 +1474,7 @@ extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc,
   const long items = (long)M * (NO / 4);
   const dim3 grid((unsigned)((items + 255) / 256));
   switch (epi) {
+    case PG_EPI_F32: hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_F32>), grid, dim3(256), 0, stream, part, nsplit, e); break;
     case PG_EPI_BF16: hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16>), grid, dim3(256), 0, stream, part, nsplit, e); break;
     case PG_EPI_BF16_GELU: hipLaunchKernelGGL((gemm_finalize_kernel<PG_EPI_BF16_GELU>), grid, dim3(256), 0, stream, part, nsplit, e); break;
     case PG_EPI_BF16_GELU_MUL:

@@ -69,6 +69,7 @@ class PaliGemmaEngine:
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
     ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
+    TAIL_SPLIT = os.environ.get("PG_TAIL_SPLIT", "1") != "0"   # ... the tail with its own deeper split-K
     # ragged-N SigLIP GEMMs as head + tail launches: measured neutral at pt-448 x16 and pt-896 x32 (the small-tile
     # tail costs what the saved round gave back; scripts/tune/run_s4_p.sh), so off
     COL_BLOCKS = os.environ.get("PG_COL_BLOCKS", "0") == "1"
@@ -262,8 +263,19 @@ class PaliGemmaEngine:
                 # Both write the same [ksplit][M][N] slabs (PgFusedArgs.slab_rows)
                 fr = ops.fused_args(slab_rows=M)
                 ops.gemm_fused(x[:Mh], W, out, fr, epi=epi | flag, M=Mh, ksplit=ksplit, ldc=out.stride(-2))
+                N, K, Mt = W.shape[0], W.shape[1], M - Mh
+                st = max(ksplit, ops.split_for(math.ceil(Mt / 64) * math.ceil(N / 128), K // 64, max_split=8))
+                if st > ksplit and self.TAIL_SPLIT:
+                    # the tail's own deeper split (its 64x128 tiles alone leave most CUs idle), summed into
+                    # slab 0's tail rows; the other slabs' tail rows are zeroed (the head never writes them)
+                    tp = self._buf("row_tail", (st, Mt, N), torch.float32)
+                    ops.gemm(x[Mh:M], W, tp, epi=epi | flag, ksplit=st)
+                    ops.slab_sum(tp, out[0, Mh:M])
+                    if ksplit > 1:
+                        out[1:ksplit, Mh:M].zero_()
+                    return out
                 tail = out.view(-1)[Mh * out.stride(-2):]
-                return ops.gemm_fused(x[Mh:M], W, tail, fr, epi=epi | flag, M=M - Mh, ksplit=ksplit,
+                return ops.gemm_fused(x[Mh:M], W, tail, fr, epi=epi | flag, M=Mt, ksplit=ksplit,
                                       ldc=out.stride(-2))
         if fa is not None:
             return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)

@@ -317,6 +317,17 @@ def finalize_split(M: int, N: int, K: int) -> int:
     return s if s >= 2 else 1
 
 
+def slab_sum(part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[M][N] (fp32, row stride out.stride(0)) = sum over the slabs of part[s][M][N] (pg_gemm_finalize, PG_EPI_F32)."""
+    _chk(part, torch.float32, "part")
+    _chk(out, torch.float32, "out")
+    S, M, N = part.shape
+    if not part.is_contiguous() or out.shape != (M, N) or out.stride(1) != 1:
+        raise ValueError("pghip.slab_sum: part must be contiguous [S][M][N] and out [M][N] with unit column stride")
+    _lib.call("pg_gemm_finalize", _p(part), S, _p(out), out.stride(0), M, N, EPI_F32, None, 0, 0, None, _s())
+    return out
+
+
 def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -> int:
     """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
     s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))

@@ -86,6 +86,15 @@ def test_gemm_slab_rows_row_blocks(M, N, K, s):
     assert torch.equal(two[:, :Mh], one[:, :Mh])        # the head's tiles are the same launches' tiles
 
 
+def test_slab_sum_into_strided_rows():
+    from pghip import ops
+    part = torch.randn(5, 40, 64).cuda()
+    out = torch.full((3, 100, 64), 7.0, device="cuda")
+    ops.slab_sum(part, out[0, 60:])
+    assert torch.allclose(out[0, 60:], part.sum(0), atol=1e-6, rtol=0)
+    assert (out[0, :60] == 7.0).all() and (out[1:] == 7.0).all()
+
+
 @pytest.mark.parametrize("M,N,K,epi,s", [(300, 300, 128, "gelu", 1), (300, 300, 128, "f32", 2),
                                          (16384, 1152, 1152, "f32", 1), (16384, 4304, 1152, "gelu", 1)])
 def test_gemm_column_blocks(M, N, K, epi, s):
