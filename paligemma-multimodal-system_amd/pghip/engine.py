@@ -70,6 +70,7 @@ class PaliGemmaEngine:
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
     ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
     TAIL_SPLIT = os.environ.get("PG_TAIL_SPLIT", "1") != "0"   # ... the tail with its own deeper split-K
+    HEAD_KSPLIT = os.environ.get("PG_HEAD_KSPLIT", "1") != "0"  # ... and the split-K chosen for the head
     # ragged-N SigLIP GEMMs as head + tail launches: measured neutral at pt-448 x16 and pt-896 x32 (the small-tile
     # tail costs what the saved round gave back; scripts/tune/run_s4_p.sh), so off
     COL_BLOCKS = os.environ.get("PG_COL_BLOCKS", "0") == "1"
@@ -235,8 +236,18 @@ class PaliGemmaEngine:
         return self.fp8 and M > 16
 
     def _ksplit(self, M: int, N: int, K: int) -> int:
-        """split-K of an fp32-partial GEMM (fp8 operands: the kernels count K in byte pairs)."""
-        return ops.gemm_ksplit(M, N, K // 2 if self._fp8_rows(M) else K)
+        """split-K of an fp32-partial GEMM (fp8 operands: the kernels count K in byte pairs).  A GEMM that will
+        run as row blocks (_lin / _row_head) takes the split that suits its whole-tile head: the pt-448 x16
+        down projection then runs 512 full-K tiles in 2 rounds instead of 1536 third-K tiles in 6, and two
+        fewer fp32 slabs are written and re-read by the next RMSNorm."""
+        if self._fp8_rows(M):
+            return ops.gemm_ksplit(M, N, K // 2)
+        Mh = M // 256 * 256
+        if self.ROW_BLOCKS and self.HEAD_KSPLIT and 0 < Mh < M:
+            s = ops.gemm_ksplit(Mh, N, K)
+            if self._row_head(M, N, s):
+                return s
+        return ops.gemm_ksplit(M, N, K)
 
     def _lin(self, x: torch.Tensor, Lw: dict, name: str, out: torch.Tensor, epi: int, M: int, ksplit: int = 1,
              fa=None):
