@@ -71,6 +71,7 @@ class PaliGemmaEngine:
     ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
     TAIL_SPLIT = os.environ.get("PG_TAIL_SPLIT", "1") != "0"   # ... the tail with its own deeper split-K
     HEAD_KSPLIT = os.environ.get("PG_HEAD_KSPLIT", "1") != "0"  # ... and the split-K chosen for the head
+    ROW_BLOCKS_GU = os.environ.get("PG_ROW_BLOCKS_GU", "1") != "0"  # gate/up (bf16 gelu*up) as row blocks too
     # ragged-N SigLIP GEMMs as head + tail launches: measured neutral at pt-448 x16 and pt-896 x32 (the small-tile
     # tail costs what the saved round gave back; scripts/tune/run_s4_p.sh), so off
     COL_BLOCKS = os.environ.get("PG_COL_BLOCKS", "0") == "1"
@@ -288,6 +289,11 @@ class PaliGemmaEngine:
                 tail = out.view(-1)[Mh * out.stride(-2):]
                 return ops.gemm_fused(x[Mh:M], W, tail, fr, epi=epi | flag, M=Mt, ksplit=ksplit,
                                       ldc=out.stride(-2))
+        if fa is None and epi == ops.EPI_BF16_GELU_MUL and self.ROW_BLOCKS and self.ROW_BLOCKS_GU:
+            Mh = self._row_head(M, W.shape[0], 1)
+            if Mh:      # gate/up at pt-448 x16: 8192 whole tiles (32 rounds) + a 128-row tail, not 33 rounds
+                ops.gemm(x[:Mh], W, out[:Mh], epi=epi | flag)
+                return ops.gemm(x[Mh:M], W, out[Mh:M], epi=epi | flag)
         if fa is not None:
             return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)
         return ops.gemm(x, W, out, epi=epi | flag, ksplit=ksplit)
