@@ -25,6 +25,9 @@
 #ifndef PG_FA_W12
 #define PG_FA_W12 1       // prefill, head_dim 256: 12-wave workgroups when they fill the one-per-CU rounds better
 #endif
+#ifndef PG_COMBINE_PF
+#define PG_COMBINE_PF 12  // split-KV merge: O partials of the first 12 splits per thread loaded up front
+#endif
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
@@ -545,6 +548,15 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   const int b = bk / Hkv, kvh = bk % Hkv;
   __shared__ float wsh[256];
   __shared__ float inv_den;
+  // thread (sg, dq): dims 4dq..4dq+3, splits sg, sg+4, ...; the first PG_COMBINE_PF of its splits' O partials
+  // are loaded before the (m, l) reduction (clamped addresses, discarded by a select later), so the usual
+  // split count (<= 4 * PG_COMBINE_PF) costs one memory round trip instead of two
+  const int dq = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  const bool dok = 4 * dq < D;
+  const float* po = part_o + ((long)bk * nsplit * 16 + row) * DTW + 4 * (dok ? dq : 0);
+  f32x4 pre[PG_COMBINE_PF > 0 ? PG_COMBINE_PF : 1];
+#pragma unroll
+  for (int i = 0; i < PG_COMBINE_PF; ++i) pre[i] = *(const f32x4*)(po + (long)min(sg + 4 * i, nsplit - 1) * 16 * DTW);
   // split weights 2^(m_s - M) (thread s), and the denominator
   float ms = -INFINITY, ls = 0.f;
   if ((int)threadIdx.x < nsplit) {
@@ -565,14 +577,18 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   __syncthreads();
   if (threadIdx.x == 0) inv_den = 1.0f / (red[0] + red[1] + red[2] + red[3]);
   __syncthreads();
-  // thread (sg, dq): dims 4dq..4dq+3, splits sg, sg+4, ... (16-B loads, 4 independent streams per dim
-  // group, no branch around a load); the four split groups are summed in LDS
-  const int dq = threadIdx.x & 63, sg = threadIdx.x >> 6;
+  // (16-B loads, 4 independent streams per dim group, no branch around a load); the four split groups are
+  // summed in LDS
   f32x4 num = {0.f, 0.f, 0.f, 0.f};
-  if (4 * dq < D) {
-    const float* po = part_o + ((long)bk * nsplit * 16 + row) * DTW + 4 * dq;
+  if (dok) {
+#pragma unroll
+    for (int i = 0; i < PG_COMBINE_PF; ++i) {
+      const int s2 = sg + 4 * i;
+      const float wv = s2 < nsplit ? wsh[s2] : 0.f;
+      num += wv != 0.f ? wv * pre[i] : f32x4{0.f, 0.f, 0.f, 0.f};   // empty splits hold no partials
+    }
 #pragma unroll 4
-    for (int s2 = sg; s2 < nsplit; s2 += 4) {
+    for (int s2 = sg + 4 * PG_COMBINE_PF; s2 < nsplit; s2 += 4) {
       const float wv = wsh[s2];
       const f32x4 pv = *(const f32x4*)(po + (long)s2 * 16 * DTW);
       num += wv != 0.f ? wv * pv : f32x4{0.f, 0.f, 0.f, 0.f};   // empty splits hold no partials
