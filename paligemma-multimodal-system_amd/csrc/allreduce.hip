@@ -11,11 +11,15 @@
 // Exchange buffer of one rank (uncached device memory, mapped into the peers with IPC handles):
 //   [0, 4096)   flags   u32 [2 sets][PG_XG_MAXWG workgroups][PG_XG_MAXW ranks]
 //   [4096, ..)  slots   f32 [2 sets][W][cap]
-// Call e (per workgroup, counted in a local `epochs[wg]` word) uses set e&1 and raises its flags to
-// e.  A rank can only start call e+2 after every peer raised its flags for e+1, i.e. after every
-// peer finished reading set e&1 for call e, so two sets make the reuse race-free.  Everything the
-// kernel needs lives on the device (epoch counters included), so the call is capturable into the
-// decode hipGraph.
+// Every call launches all PG_XG_MAXWG workgroups and workgroup w always owns the same elements: the
+// fixed PG_XG_CHUNK-float chunks w, w + PG_XG_MAXWG, w + 2*PG_XG_MAXWG, ... (a grid-stride loop; a
+// workgroup with no chunk below n still does the flag handshake).  So every workgroup's local epoch
+// counter `epochs[wg]` advances on every call, all workgroups agree on the call count e, and call e uses
+// buffer set e&1.  A rank starts call e+2 only after its call e+1 finished, which needed every peer's
+// flags for e+1; a peer raises those only after its call e (which read set e&1) finished (stream order).
+// So the two sets make slot reuse race-free for any sequence of sizes, without a host sync between
+// calls.  Everything the kernel needs lives on the device (epoch counters included), so the call is
+// capturable into the decode hipGraph.
 //
 // Waiting is bounded by the 100 MHz wall clock: a peer that never arrives sets err[0] and the kernel
 // finishes (its output is then meaningless) instead of hanging the device.
@@ -25,6 +29,7 @@
 
 #define PG_XG_MAXW 8
 #define PG_XG_MAXWG 64
+#define PG_XG_CHUNK 8192                    // floats per chunk (32 KB)
 #define PG_XG_FLAG_BYTES 4096
 #define PG_XG_TIMEOUT_TICKS 2000000000ull   // 20 s of the 100 MHz constant clock
 
@@ -33,7 +38,7 @@ struct XgPeers {
 };
 
 template <int W>
-__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__ data, long chunk, long n, int rank,
+__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__ data, long n, int rank,
                                                              XgPeers peers, long cap, unsigned* __restrict__ epochs,
                                                              int* __restrict__ err) {
   const int wg = blockIdx.x, tid = threadIdx.x;
@@ -41,15 +46,18 @@ __global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__
   __syncthreads();
   if (tid == 0) epochs[wg] = e;
   const int set = (int)(e & 1u);
-  const long c0 = (long)wg * chunk, c1 = c0 + chunk < n ? c0 + chunk : n;
+  constexpr long STRIDE = (long)PG_XG_MAXWG * PG_XG_CHUNK;
 
-  // 1. push this rank's chunk into slot `rank` of every peer (and of itself)
-  for (long i = c0 + 4 * tid; i < c1; i += 1024) {
-    const f32x4 v = *(const f32x4*)(data + i);
+  // 1. push this rank's chunks into slot `rank` of every peer (and of itself)
+  for (long c0 = (long)wg * PG_XG_CHUNK; c0 < n; c0 += STRIDE) {
+    const long c1 = c0 + PG_XG_CHUNK < n ? c0 + PG_XG_CHUNK : n;
+    for (long i = c0 + 4 * tid; i < c1; i += 1024) {
+      const f32x4 v = *(const f32x4*)(data + i);
 #pragma unroll
-    for (int p = 0; p < W; ++p) {
-      float* dst = (float*)((char*)peers.p[p] + PG_XG_FLAG_BYTES) + ((long)set * W + rank) * cap + i;
-      __builtin_nontemporal_store(v, (f32x4*)dst);
+      for (int p = 0; p < W; ++p) {
+        float* dst = (float*)((char*)peers.p[p] + PG_XG_FLAG_BYTES) + ((long)set * W + rank) * cap + i;
+        __builtin_nontemporal_store(v, (f32x4*)dst);
+      }
     }
   }
   __threadfence_system();   // this thread's slot stores are complete and visible system-wide
@@ -59,7 +67,7 @@ __global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__
     __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 
-  // 2. wait for the W flags of this workgroup's chunk in the local buffer
+  // 2. wait for the W flags of this workgroup's chunks in the local buffer
   if (tid < W) {
     unsigned* f = (unsigned*)peers.p[rank] + (set * PG_XG_MAXWG + wg) * PG_XG_MAXW + tid;
     const unsigned long long t0 = wall_clock64();
@@ -76,11 +84,14 @@ __global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__
 
   // 3. sum the W slots in rank order (identical on every rank)
   const float* slots = (const float*)((const char*)peers.p[rank] + PG_XG_FLAG_BYTES) + (long)set * W * cap;
-  for (long i = c0 + 4 * tid; i < c1; i += 1024) {
-    f32x4 s = __builtin_nontemporal_load((const f32x4*)(slots + i));
+  for (long c0 = (long)wg * PG_XG_CHUNK; c0 < n; c0 += STRIDE) {
+    const long c1 = c0 + PG_XG_CHUNK < n ? c0 + PG_XG_CHUNK : n;
+    for (long i = c0 + 4 * tid; i < c1; i += 1024) {
+      f32x4 s = __builtin_nontemporal_load((const f32x4*)(slots + i));
 #pragma unroll
-    for (int p = 1; p < W; ++p) s += __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
-    *(f32x4*)(data + i) = s;
+      for (int p = 1; p < W; ++p) s += __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
+      *(f32x4*)(data + i) = s;
+    }
   }
 }
 
@@ -97,6 +108,9 @@ extern "C" int pg_xgmi_alloc(long bytes, void** out) {
   hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   e = hipMemset(p, 0, (size_t)bytes);
+  // the zeroing must be complete before the IPC handle is exported and a peer's first flag or slot
+  // store can land (a late memset would wipe it and the exchange would time out)
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     (void)hipFree(p);
     return (int)e;
@@ -139,13 +153,10 @@ extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void*
     PG_REQUIRE(peers[r] != nullptr && ((uintptr_t)peers[r] & 15) == 0);
     pp.p[r] = peers[r];
   }
-  // 8192 floats (32 KB) per workgroup at least, at most PG_XG_MAXWG workgroups
-  long chunk = (n + PG_XG_MAXWG - 1) / PG_XG_MAXWG;
-  chunk = chunk < 8192 ? 8192 : (chunk + 3) / 4 * 4;
-  const int wgs = (int)((n + chunk - 1) / chunk);
+  // always the full grid: every workgroup's epoch advances on every call (see the header)
 #define PG_XG_CASE(WW)                                                                                       \
   case WW:                                                                                                   \
-    hipLaunchKernelGGL((allreduce_xgmi_kernel<WW>), dim3(wgs), dim3(256), 0, stream, data, chunk, n, rank, pp, \
+    hipLaunchKernelGGL((allreduce_xgmi_kernel<WW>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n, rank, pp, \
                        cap, epochs, err);                                                                    \
     break;
   switch (world) {

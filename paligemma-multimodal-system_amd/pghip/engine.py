@@ -626,9 +626,17 @@ class PaliGemmaEngine:
             sampler["uniforms"] = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
         self.sample(logits, st, sampler, advance=False)                  # token 1 from the prefill logits
         n = 1
-        use_graph = use_graph and self.comm.capturable
-        step_fn = self._graph_step(st, cache, feats, sampler) if use_graph else \
-            (lambda: self.decode_step(st, cache, feats, sampler))
+        step_fn = None
+        if use_graph and self.comm.capturable:
+            try:
+                step_fn = self._graph_step(st, cache, feats, sampler)
+            except RuntimeError:
+                # a collective that cannot be captured (e.g. an all-reduce larger than the xGMI exchange
+                # buffer): _graph_step restored the state before capturing, so run eager steps instead
+                torch.cuda.synchronize()
+                step_fn = None
+        if step_fn is None:
+            step_fn = lambda: self.decode_step(st, cache, feats, sampler)  # noqa: E731
         while n < max_new_tokens:
             if stop_token is not None and n % check_every == 0:
                 if B == 1:
@@ -639,6 +647,8 @@ class PaliGemmaEngine:
             step_fn()
             n += 1
         hist = st["hist"][:n].t().contiguous().cpu()
+        if hasattr(self.comm, "check"):
+            self.comm.check()              # an xGMI exchange that timed out leaves meaningless sums: raise
         if stop_token is None:
             return [r.tolist() for r in hist] if return_list else hist
         rows = []

@@ -37,8 +37,10 @@ class XgmiComm(TPComm):
 
     Every rank holds one exchange buffer; the handles travel through all_gather_object, so this also
     works over gloo (two ranks sharing one device in the tests).  Because the kernel keeps its epoch
-    counters on the device, the exchange is graph-capturable whatever the backend: `capturable` is
-    True when every all-reduce the engine issues fits (`fits(numel)`)."""
+    counters on the device, the exchange is graph-capturable whatever the backend, so `capturable` is
+    True.  An all-reduce that does not fit the exchange buffer (`fits(numel)` False, e.g. the top-p
+    lm_head gather at a large batch) raises inside a capture; PaliGemmaEngine.generate and bench.py then
+    fall back to eager decode steps."""
 
     def __init__(self, group=None, cap: int = 1 << 22):
         super().__init__(group)

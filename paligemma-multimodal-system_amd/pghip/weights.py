@@ -127,6 +127,13 @@ class PackedWeights:
         for i in range(self.v_layers):
             lp = f"{pre}encoder.layers.{i}."
             a = lp + "self_attn."
+            for nm in ("q_proj.bias", "k_proj.bias", "v_proj.bias", "o_proj.bias"):
+                try:
+                    b = get(a + nm)
+                except KeyError:
+                    continue
+                if b is not None:
+                    raise NotImplementedError(f"{a + nm}: Gemma attention biases are not supported by the HIP path")
             qkv_w = torch.cat([bf(get(a + "query_proj.weight")), bf(get(a + "key_proj.weight")),
                                bf(get(a + "value_proj.weight"))], 0).contiguous()
             qkv_b = torch.cat([f32(get(a + "query_proj.bias")), f32(get(a + "key_proj.bias")),
@@ -167,6 +174,10 @@ class PackedWeights:
             raise ValueError(f"vocab_size {self.vocab} does not split over {W} ranks")
         if self.head_dim % 16:
             raise ValueError("head_dim must be a multiple of 16 for the fused RoPE epilogue")
+        if t.get("attention_bias"):
+            # GemmaAttention creates q/k/v/o biases when attention_bias is set (modeling_gemma.py:255-259) and
+            # the reference adds them; the HIP q|k|v and o epilogues carry none, so refuse rather than diverge
+            raise NotImplementedError("attention_bias=True is not supported by the HIP Gemma path")
         self.heads = self.heads_total // W                    # q heads held by this rank
         self.inter_real = self.inter_total // W               # intermediate slice held by this rank
         self.inter = _rup(self.inter_real, 128 if self.fp8 else 64)   # kernel width: zero-padded to the GEMM K step
@@ -202,6 +213,13 @@ class PackedWeights:
         for i in range(self.t_layers):
             lp = f"{lm}model.layers.{i}."
             a = lp + "self_attn."
+            for nm in ("q_proj.bias", "k_proj.bias", "v_proj.bias", "o_proj.bias"):
+                try:
+                    b = get(a + nm)
+                except KeyError:
+                    continue
+                if b is not None:
+                    raise NotImplementedError(f"{a + nm}: Gemma attention biases are not supported by the HIP path")
             qkv_w = torch.cat([bf(get(a + "q_proj.weight")[q_lo:q_hi]), bf(get(a + "k_proj.weight")),
                                bf(get(a + "v_proj.weight"))], 0)
             qkv_w = qkv_w.view(nblk, hd, H)[:, perm, :].reshape(nblk * hd, H).contiguous()

@@ -157,3 +157,19 @@ def test_packed_weights_frag_flags():
     assert np.array_equal(lm, W["language_model.model.embed_tokens.weight"].astype(np.float32))
     P4 = PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu", parts=("text",), tp_rank=1, tp_world=4)
     assert not P4.frag and P4.wflag == 0
+
+
+def test_packed_weights_refuse_attention_bias():
+    """GemmaAttention with attention_bias=True adds q/k/v/o biases (modeling_gemma.py:295-298); the HIP q|k|v and
+    o epilogues carry none, so packing must fail loudly instead of silently dropping them."""
+    import copy
+    from pghip.weights import PackedWeights
+    cfg = copy.deepcopy(ocfg.TINY)
+    W = synth.generate_state_dict(cfg)
+    cfg["text_config"]["attention_bias"] = True
+    with pytest.raises(NotImplementedError):
+        PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu", parts=("text",))
+    cfg["text_config"]["attention_bias"] = False
+    Wb = dict(W, **{"language_model.model.layers.0.self_attn.q_proj.bias": np.zeros(1, np.float32)})
+    with pytest.raises(NotImplementedError):
+        PackedWeights(cfg, lambda k: torch.from_numpy(Wb[k]), device="cpu", parts=("text",))

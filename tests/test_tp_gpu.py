@@ -36,7 +36,8 @@ def _launch(worker, tmp_path, **env):
 def test_xgmi_allreduce_two_ranks_on_one_device(tmp_path):
     """pg_allreduce_xgmi between two processes sharing the device through IPC-mapped exchange buffers:
     bit-exact against the rank-order fp32 sum for ragged sizes (one and many workgroups, both buffer
-    sets), identical on both ranks, inside a captured hipGraph, and without a timeout."""
+    sets), back to back with different sizes and no host sync, identical on both ranks, inside a captured
+    hipGraph, and without a timeout."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
     res = _launch("xgmi_worker.py", tmp_path)
@@ -44,6 +45,7 @@ def test_xgmi_allreduce_two_ranks_on_one_device(tmp_path):
         assert o["err"] == 0, o
         assert o["bad"] == [], o
         assert o["graph_bad"] == [], o
+        assert o["seq_bad"] == [], o
     assert res[0]["digest"] == res[1]["digest"]
 
 

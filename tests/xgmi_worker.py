@@ -39,6 +39,16 @@ def main():
         if not torch.equal(got, expected(n, world, it)):
             bad.append([n, it, float((got - expected(n, world, it)).abs().max())])
         dig.update(got.numpy().tobytes())
+    # back to back without a host sync: one-chunk, multi-chunk-per-workgroup and cap-sized exchanges
+    # interleaved, so a workgroup that reused a buffer set early would corrupt a peer's unread slots
+    seq = [2048, 600000, 4, 1 << 20, 2048, 524292, 8196, 1 << 20]
+    ins = [rank_data(n, rank, 200 + i).cuda() for i, n in enumerate(seq)]
+    torch.cuda.synchronize()
+    dist.barrier()
+    for t in ins:
+        comm.all_reduce(t)
+    torch.cuda.synchronize()
+    seq_bad = [[n, i] for i, (n, t) in enumerate(zip(seq, ins)) if not torch.equal(t.cpu(), expected(n, world, 200 + i))]
     # captured: three exchanges of different sizes in one graph, replayed with fresh inputs
     sizes = [2048, 2048 * 16, 4 * 8192]
     static = [torch.zeros(n, device="cuda") for n in sizes]
@@ -62,7 +72,7 @@ def main():
         for t, n in zip(static, sizes):
             if not torch.equal(t.cpu(), expected(n, world, it)):
                 graph_bad.append([n, rep])
-    out = {"rank": rank, "err": int(comm.err.item()), "bad": bad, "graph_bad": graph_bad,
+    out = {"rank": rank, "err": int(comm.err.item()), "bad": bad, "graph_bad": graph_bad, "seq_bad": seq_bad,
            "digest": dig.hexdigest()}
     del g
     comm.close()
