@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);
+int pg_abi_version(void);   /* 2: pg_attention takes kcap */
 
 /* Epilogues of pg_gemm */
 enum {
@@ -131,12 +131,13 @@ int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part
 
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
- * split-KV partials, merge with pg_attn_combine. */
+ * split-KV partials, merge with pg_attn_combine; kcap > 0 = readable cache rows (Smax, multiple of 32): each split's
+ * first block is loaded before the kv length is read (ABI 2). */
 int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
                  long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
                  long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
                  int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
-                 hipStream_t stream);
+                 int kcap, hipStream_t stream);
 int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                     void* o, long o_rs, hipStream_t stream);
 

@@ -32,6 +32,14 @@
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
 
+// Decode (split mode): one wave per (batch, kv head, split); grid (1, Hkv * nsplit, B).
+template <int DP, int DT, bool FULL>
+__global__ __launch_bounds__(64) void attn_decode_kernel(AttnArgs a) {
+  const int nsplit = (int)gridDim.y / a.Hkv;
+  attn_decode_split<DP, DT, false, FULL>(a, blockIdx.z, blockIdx.y / nsplit, blockIdx.y % nsplit, nsplit,
+                                         threadIdx.x);
+}
+
 template <int DP, int DT>
 __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   constexpr int KS = DP / 32;  // QK^T k-steps
@@ -646,6 +654,10 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
       launch_fa<DP_, DT_>(fa_waves, fa_rpw, grid, stream, a);                                \
     else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
+    else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32)           \
+      hipLaunchKernelGGL((attn_decode_kernel<DP_, DT_, true>), grid, dim3(64), 0, stream, a); \
+    else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1)                                     \
+      hipLaunchKernelGGL((attn_decode_kernel<DP_, DT_, false>), grid, dim3(64), 0, stream, a); \
     else                                                                                     \
       hipLaunchKernelGGL((attn_kernel<DP_, DT_>), grid, dim3(split_keys > 0 ? 64 * PG_ATTN_SPLIT_WAVES : 64), 0, \
                          stream, a);                                                         \
@@ -657,19 +669,23 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
 // vt for (b, d, key, kvh): vt + b*vt_bs + kvh*vt_hs + d*vt_ds + key.  mask (optional, additive fp32): mask + b*mask_bs
 // + pos*mask_rs + key.  Lkv = (lkv_dev ? *lkv_dev : 0) + Lkv.
 // split_keys == 0: prefill mode (writes bf16 o).  split_keys > 0: decode mode, Lq*Hq/Hkv <= 16, nsplit partials
-// (nsplit multiple of 4) to part_o / part_ml, then call pg_attn_combine.
+// (nsplit multiple of 4) to part_o / part_ml, then call pg_attn_combine.  kcap > 0 (decode): K rows and V^T
+// columns [0, kcap) are readable (a static cache's Smax, a multiple of 32), so each split issues its first block's
+// loads before the kv length arrives from lkv_dev; 0 = rows clamped to the kv length.
 extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
                             long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
                             long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
                             int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
-                            hipStream_t stream) {
+                            int kcap, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && D > 0 && D % 8 == 0 && D <= 256);
+  PG_REQUIRE(kcap >= 0 && kcap % 32 == 0);
   const int G = Hq / Hkv;
   const int DP = ((D + 31) / 32) * 32;
   const int DT = (D + 15) / 16;
   AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, (const bf16_t*)k, k_bs, k_hs, k_rs,
              (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, mask, mask_bs, mask_rs,
-             Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml};
+             Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml,
+             split_keys > 0 ? kcap : 0};
   dim3 grid;
   // prefill with >= 1024 one-wave workgroups: the LDS-staged kernel (64 rows per workgroup share K/V);
   // needs 16-B aligned V^T rows / batch offsets

@@ -15,6 +15,8 @@ struct AttnArgs {
   int split_keys;          // split mode if > 0 (keys per wave)
   float* part_o;           // [B][Hkv][nsplit][16][DT*16]
   float* part_ml;          // [B][Hkv][nsplit][16][2]
+  int kcap;                // decode: key rows readable per (b, kv head) in K and V^T (the static cache's Smax);
+                           // > 0 lets a split issue its first block's loads before the kv length arrives
 };
 
 // Branch-free guarded loads: the address is always valid (callers clamp it), the value is
@@ -59,19 +61,25 @@ static __device__ __forceinline__ f32x2 ld8_wt(const float* p) {
 // the q rows r < Lq*G (Lq == 1: row r = q head kvh*G + r), written as (O, m, l) partials of split sp of nsplit.
 // S^T = K.Q^T keeps each row's softmax statistics lane-local; O^T = V^T.P^T takes P from the S accumulators
 // (key order permuted identically for V^T).  WT: write-through stores for a consumer inside the same launch.
-template <int DP, int DT, bool WT>
+// FULL (head_dim == DP): no lane-dependent selects on loaded values -- rows past Lq*G read row Lq*G-1 (never
+// stored) -- so hipcc has no reason to wait for a load before the next one is issued, and the kv length is
+// read with a vector load (in order with the stream; a scalar load's lgkmcnt wait lands before the first
+// vector load, behind the kernel-argument loads).
+template <int DP, int DT, bool WT, bool FULL = false>
 __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int kvh, int sp, int nsplit, int lane) {
   constexpr int KS = DP / 32;
   const int c = lane & 15, g = lane >> 4;
-  const int Lkv = (a.lkv_dev ? *a.lkv_dev : 0) + a.Lkv;
   const int R = a.Lq * a.G;
-  const int D = a.D;
+  const int D = FULL ? DP : a.D;
   const int kbeg = sp * a.split_keys;
-  const int kend = min(Lkv, kbeg + a.split_keys);
   const int r = c;
   const bool rvalid = r < R;
-  const int pos = rvalid ? r / a.G : 0;
-  const int hq = kvh * a.G + (rvalid ? r % a.G : 0);
+  const int rr = rvalid ? r : (FULL ? R - 1 : 0);
+  const int pos = rr / a.G;
+  const int hq = kvh * a.G + rr % a.G;
+  int lkv_raw = 0;
+  if constexpr (FULL)
+    lkv_raw = __hip_atomic_load(a.lkv_dev ? a.lkv_dev : &pg_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   bf16x8 qf[KS];
   {
@@ -79,7 +87,10 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int d0 = 32 * s + 8 * g;
-      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
+      if constexpr (FULL)
+        qf[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qp + d0));
+      else
+        qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
     }
   }
   const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
@@ -88,29 +99,58 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
-  for (int kb = kbeg; kb < kend; kb += 32) {
-    // every load of the block first (K rows for S^T, V^T rows for P.V): one memory round trip
-    const int ka = min(kb + c, kend - 1), kbk = min(kb + 16 + c, kend - 1);
-    u32x4 kfa[KS], kfb[KS];
-    {
-      const bf16_t* pa = kbase + (long)ka * a.k_rs;
-      const bf16_t* pb = kbase + (long)kbk * a.k_rs;
+  // raw loads of one 32-key block: K rows for S^T (rows clamped below rowcap), 4-key runs of the V^T rows
+  // (row padded to a multiple of 32 keys); masking by the kv length is applied after the loads land
+  auto load_block = [&](int kb, int rowcap, u32x4 (&kfa)[KS], u32x4 (&kfb)[KS], u32x2 (&vr)[DT][2]) {
+    const int ka = min(kb + c, rowcap - 1), kbk = min(kb + 16 + c, rowcap - 1);
+    const bf16_t* pa = kbase + (long)ka * a.k_rs;
+    const bf16_t* pb = kbase + (long)kbk * a.k_rs;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int d0 = 32 * s + 8 * g;
+    for (int s = 0; s < KS; ++s) {
+      const int d0 = 32 * s + 8 * g;
+      if constexpr (FULL) {
+        kfa[s] = *(const u32x4*)(pa + d0);
+        kfb[s] = *(const u32x4*)(pb + d0);
+      } else {
         kfa[s] = ld16_sel(pa + (d0 < D ? d0 : 0), d0 < D);
         kfb[s] = ld16_sel(pb + (d0 < D ? d0 : 0), d0 < D);
       }
     }
-    u32x4 vf[DT];
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const int d = 16 * t + c;
-      const bool dok = d < D;
-      const bf16_t* vrow = vbase + (long)(dok ? d : D - 1) * a.vt_ds;
-      const u32x2 v0 = ld_vt4(vrow, kb + 4 * g, kend, dok);
-      const u32x2 v1 = ld_vt4(vrow, kb + 16 + 4 * g, kend, dok);
-      vf[t] = u32x4{v0[0], v0[1], v1[0], v1[1]};
+      const bf16_t* vrow = vbase + (long)(d < D ? d : D - 1) * a.vt_ds;
+      vr[t][0] = *(const u32x2*)(vrow + kb + 4 * g);
+      vr[t][1] = *(const u32x2*)(vrow + kb + 16 + 4 * g);
+    }
+  };
+  // decode with a known cache capacity: the first block is in flight before the kv length is read.  FULL
+  // (launched only with kcap > 0) loads it unconditionally -- a split past the cache reads the last block,
+  // never used -- so no branch joins the loads (hipcc's wait bookkeeping stays exact)
+  const bool pre = FULL || (a.kcap > 0 && kbeg < a.kcap);
+  u32x4 kfa[KS], kfb[KS];
+  u32x2 vr[DT][2];
+  if (FULL) load_block(min(kbeg, a.kcap - 32), a.kcap, kfa, kfb, vr);
+  else if (pre) load_block(kbeg, a.kcap, kfa, kfb, vr);
+  const int Lkv = (FULL ? __builtin_amdgcn_readfirstlane(lkv_raw) : (a.lkv_dev ? *a.lkv_dev : 0)) + a.Lkv;
+  const int kend = min(Lkv, kbeg + a.split_keys);
+  // one 32-key block from the loaded registers: mask by the kv length, S^T, online softmax, P.V.  A block with
+  // no valid key (a peeled first block past the kv length) leaves (o, m, l) = (0, -inf, 0) untouched.
+  auto block = [&](int kb) {
+    // every load of the block is issued before its first use (one memory round trip): the scheduler would
+    // otherwise sink the V^T loads below the S^T MFMAs, behind the K loads' wait
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 vf[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const bool dok = 16 * t + c < D;
+      const int k0 = kb + 4 * g, k1 = kb + 16 + 4 * g;
+      const int n0 = dok ? kend - k0 : 0, n1 = dok ? kend - k1 : 0;   // valid keys among each run of 4
+      const u32x2 v0 = vr[t][0], v1 = vr[t][1];
+      vf[t] = u32x4{n0 >= 2 ? v0[0] : (n0 == 1 ? (v0[0] & 0xFFFFu) : 0u),
+                    n0 >= 4 ? v0[1] : (n0 == 3 ? (v0[1] & 0xFFFFu) : 0u),
+                    n1 >= 2 ? v1[0] : (n1 == 1 ? (v1[0] & 0xFFFFu) : 0u),
+                    n1 >= 4 ? v1[1] : (n1 == 3 ? (v1[1] & 0xFFFFu) : 0u)};
     }
     f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -131,10 +171,11 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
     bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
     const float mn = fmaxf(m, bm);
-    const float alpha = exp2f(m - mn);
+    const bool none = mn == -INFINITY;          // every key of the block masked and nothing before it
+    const float alpha = none ? 1.f : exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { x[j] = exp2f(x[j] - mn); rs += x[j]; }
+    for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
@@ -149,6 +190,20 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
 #pragma unroll
     for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, o[t]);
+  };
+  if constexpr (FULL) {
+    // the prefetched first block runs unconditionally (straight-line from its loads: nothing for hipcc to sink
+    // below a kv-length branch), later blocks of a multi-block split load as they go
+    block(kbeg);
+    for (int kb = kbeg + 32; kb < kend; kb += 32) {
+      load_block(kb, kend, kfa, kfb, vr);
+      block(kb);
+    }
+  } else {
+    for (int kb = kbeg; kb < kend; kb += 32) {
+      if (!pre || kb != kbeg) load_block(kb, kend, kfa, kfb, vr);
+      block(kb);
+    }
   }
   // lane holds O^T[d = 16t + 4g + j][q = c]
   const long base = (((long)b * a.Hkv + kvh) * nsplit + sp) * 16 + c;

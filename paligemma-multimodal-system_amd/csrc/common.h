@@ -79,6 +79,10 @@ __device__ __forceinline__ float block_sum(float v, float* red /* >= 16 floats o
   return s;
 }
 
+// a zero word in device memory: read in place of an absent optional device-side scalar, so the load is
+// unconditional (no branch or select on a loaded value, which makes hipcc wait for it on the spot)
+static __device__ int pg_zero_word = 0;
+
 // error reporting: every C entry point returns a hipError_t as int (0 = ok)
 #define PG_LAUNCH_CHECK() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
 #define PG_REQUIRE(cond) do { if (!(cond)) return (int)hipErrorInvalidValue; } while (0)

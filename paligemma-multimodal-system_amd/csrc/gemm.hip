@@ -128,7 +128,15 @@ __device__ __forceinline__ void scale_acc(const EpiArgs& e, int m, int n0, f32x4
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
 // the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).
 // v: columns n0..n0+3 (bias added), pr: the same four of the rotate_half partner columns (n0 ^ 8)
-__device__ __forceinline__ void epi_qkv_rope4_pr(const EpiArgs& e, int m, int n0, f32x4 v, f32x4 pr) {
+// index in [0, D/2) of column n0's rotary frequency, and whether n0 is in a q or k block (RoPE'd)
+__device__ __forceinline__ int rope_freq_index(const PgFusedArgs& f, int n0, bool* roped) {
+  const int D = f.head_dim, within = n0 % D, jj0 = within & 15;
+  *roped = n0 / D < f.q_heads + f.kv_heads;
+  return 8 * (within >> 4) + (jj0 & 7);
+}
+// the epilogue with the rotary cos/sin of its 4 columns and the cache slot base already loaded
+__device__ __forceinline__ void epi_qkv_rope4_core(const EpiArgs& e, int m, int n0, f32x4 v, f32x4 pr, f32x4 cs,
+                                                   f32x4 sn, int slot0) {
   if (m >= e.M || n0 >= e.N) return;
   const PgFusedArgs& f = e.f;
   const int D = f.head_dim, half = D >> 1;
@@ -138,14 +146,11 @@ __device__ __forceinline__ void epi_qkv_rope4_pr(const EpiArgs& e, int m, int n0
   const int ii = 8 * t + (jj0 & 7);                   // index in [0, D/2) of element 0
   const int d0 = second ? half + ii : ii;             // original dim of element 0
   const int b = m / f.rows_per_batch, i = m % f.rows_per_batch;
-  const int slot = f.slot_base + (f.slot_dev ? *f.slot_dev : 0) + i;
+  const int slot = slot0 + i;
   const bool in_cache = slot < f.smax;                // a token past the static cache is not appended
   const int Hq = f.q_heads, Hkv = f.kv_heads;
   const int KV = Hkv * D;
   if (blk < Hq + Hkv) {
-    const int p = f.pos[m];
-    const float* cs = f.cos_t + (long)p * half + ii;
-    const float* sn = f.sin_t + (long)p * half + ii;
     f32x4 y;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -165,6 +170,25 @@ __device__ __forceinline__ void epi_qkv_rope4_pr(const EpiArgs& e, int m, int n0
 #pragma unroll
     for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
   }
+}
+
+__device__ __forceinline__ void epi_qkv_rope4_pr(const EpiArgs& e, int m, int n0, f32x4 v, f32x4 pr) {
+  if (m >= e.M || n0 >= e.N) return;
+  const PgFusedArgs& f = e.f;
+  bool roped;
+  const int ii = rope_freq_index(f, n0, &roped);
+  f32x4 cs = {1.f, 1.f, 1.f, 1.f}, sn = {0.f, 0.f, 0.f, 0.f};
+  if (roped) {
+    const int p = f.pos[m];
+    const float* cp = f.cos_t + (long)p * (f.head_dim >> 1) + ii;
+    const float* sp = f.sin_t + (long)p * (f.head_dim >> 1) + ii;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cs[j] = cp[j];
+      sn[j] = sp[j];
+    }
+  }
+  epi_qkv_rope4_core(e, m, n0, v, pr, cs, sn, f.slot_base + (f.slot_dev ? *f.slot_dev : 0));
 }
 
 __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f32x4 v) {
@@ -706,6 +730,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_FRAG_NT
 #define PG_GEMV_FRAG_NT 1
 #endif
+#ifndef PG_GEMV_CPW
+#define PG_GEMV_CPW 1     // decode GEMV: straight-line chunk loop when every wave owns the same chunk count
+#endif
 #ifndef PG_MERGE_V2
 #define PG_MERGE_V2 1
 #endif
@@ -954,7 +981,11 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
   __syncthreads();
 }
 
-template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG>
+// CPW > 0: every wave owns exactly CPW chunks (launch checks K / CH / ksplit == 4 * CPW).  The chunk loop is then
+// straight-line code with unconditional loads, so hipcc's s_waitcnt bookkeeping stays exact: each chunk's MFMAs
+// wait only for that chunk (vmcnt(N), N = younger loads), instead of the conservative vmcnt(0) that the runtime
+// loop and its exec-masked loads produce at every ring turn (the ring drained before its first MFMA).
+template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG, int CPW = 0>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
                                                    const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
   constexpr int CH = U * 32;
@@ -972,7 +1003,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   const int per_z = (nch_all + gridDim.y - 1) / gridDim.y;
   const int c0 = z * per_z;
   const int nch = min(nch_all - c0, per_z);
-  const int mine = nch > wave ? (nch - wave + 3) / 4 : 0;   // chunks wave, wave+4, ...
+  const int mine = CPW > 0 ? CPW : (nch > wave ? (nch - wave + 3) / 4 : 0);   // chunks wave, wave+4, ...
 
   const bf16_t* wrow[NT];
   const bf16_t* wfrag[NT];
@@ -989,7 +1020,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 
   bf16_t* xs = (bf16_t*)dyn_smem;
   const int Kr = per_z * CH;                    // K range of this split (LDS row length)
-  const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : 0) * lda : nullptr;
+  // rows past M read row M-1 (their outputs are never stored): the x loads are unconditional, so the compiler
+  // has no select or branch to resolve and no reason to wait for them before issuing the rest of the stream
+  const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : M - 1) * lda : nullptr;
   // PRO 4 (M <= 2): wave 0 loads the producer's per-tile sums of squares before the weight stream (all
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
   // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
@@ -1007,24 +1040,28 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       if (SS16 && M > 2) {
         const int rr = min(r, M - 1);
 #pragma unroll
-        for (int k = 0; k < SSL; ++k) {
-          const int i = g + 4 * k;
-          const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
-          ssv[k] = i < e.f.ss_n ? v : 0.f;
-        }
+        for (int k = 0; k < SSL; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(g + 4 * k, e.f.ss_n - 1)];
       } else {
         const int lpr = M == 1 ? 64 : 32;
         const int rr = min(lane / lpr, M - 1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int i = lane % lpr + k * lpr;
-          const float v = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(i, e.f.ss_n - 1)];
-          ssv[k] = i < e.f.ss_n ? v : 0.f;
-        }
+        for (int k = 0; k < 4; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(lane % lpr + k * lpr, e.f.ss_n - 1)];
       }
     }
   }
-  const bf16_t* xlds = xs + (xvalid ? r : 0) * (Kr + XPAD);
+  const bf16_t* xlds = xs + (xvalid ? r : M - 1) * (Kr + XPAD);
+  // PG_EPI_QKV_ROPE: the epilogue's rotary positions and cache slot load before the weight stream, its cos/sin
+  // right after the first chunks are issued, so the epilogue starts without a dependent round trip
+  // (every wave loads them -- a few dwords -- so no divergent branch joins a loaded register, which would make
+  // the compiler wait for it right there)
+  int rope_p = 0, rope_slot_raw = 0;
+  if constexpr (EPI == PG_EPI_QKV_ROPE) {
+    rope_p = e.f.pos[r < M ? r : M - 1];
+    // a vector load (counted in order with the stream, unlike a scalar load whose wait lands early); a null
+    // slot_dev reads a zero word instead of a select on the loaded value
+    rope_slot_raw = __hip_atomic_load(e.f.slot_dev ? e.f.slot_dev : &pg_zero_word, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // element offset of a lane's 16-B piece s inside a CH-element chunk: PG_GEMV_CONTIG lays piece s of the 4
   // lane groups side by side (one load instruction = 64 contiguous bytes per row); otherwise a lane owns 16U
@@ -1068,10 +1105,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
-        xv[s] = xvalid ? *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
+        xv[s] = *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s);
     } else {
 #pragma unroll
-      for (int s = 0; s < U; ++s) xv[s] = xvalid ? *(const u32x4*)(xlds + koff + S_STRIDE * s) : u32x4{0u, 0u, 0u, 0u};
+      for (int s = 0; s < U; ++s) xv[s] = *(const u32x4*)(xlds + koff + S_STRIDE * s);
     }
   };
   constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
@@ -1081,7 +1118,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   if (prew) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
-      if (d < mine) loadw(d, wb[d]);
+      if (CPW > 0 ? d < CPW : d < mine) loadw(d, wb[d]);
   }
   if constexpr (STAGED) {
     float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
@@ -1089,24 +1126,69 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   }
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
-    if (d < mine) {
+    if (CPW > 0 ? d < CPW : d < mine) {
       if (!prew) loadw(d, wb[d]);
       loadx(d, xb[d]);
     }
-  for (int base = 0; base < mine; base += DEPTH) {
+  // PG_EPI_F32_FIN: the residual rows and norm weights the tile's last-arriving split finalises are loaded now
+  // (nothing else writes them in this launch), so the reducer's only round trip is the slab read
+  f32x4 fin_r[NT], fin_w[NT];
+  if constexpr (EPI == PG_EPI_F32_FIN) {
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      const int j = base + d;
-      if (j < mine) {
+    for (int t = 0; t < NT; ++t) {
+      const int n0 = min((tile0 + t) * 16, e.N - 16) + 4 * g;
+      fin_r[t] = *(const f32x4*)(e.f.fin_resid + (size_t)(r < M ? r : M - 1) * e.N + n0);
+      // (no select on a loaded value -- it would make the compiler wait right here: a null norm_w reads the
+      // residual row instead, unused)
+      fin_w[t] = *(const f32x4*)((e.f.norm_w ? e.f.norm_w : e.f.fin_resid) + n0);
+    }
+  }
+  f32x4 rope_cs[NT], rope_sn[NT];
+  if constexpr (EPI == PG_EPI_QKV_ROPE) {
 #pragma unroll
-        for (int s = 0; s < U; ++s) {
-          const bf16x8 xv = __builtin_bit_cast(bf16x8, xb[d][s]);
+    for (int t = 0; t < NT; ++t) {
+      bool roped;   // (v columns load a valid, unused entry: no select on the loaded values)
+      const int ii = rope_freq_index(e.f, min((tile0 + t) * 16, e.N - 16) + 4 * g, &roped);
+      const long off = (long)rope_p * (e.f.head_dim >> 1) + ii;
+      rope_cs[t] = *(const f32x4*)(e.f.cos_t + off);
+      rope_sn[t] = *(const f32x4*)(e.f.sin_t + off);
+    }
+  }
+  if constexpr (CPW > 0) {
+    // sched_barrier: the scheduler may not sink the ring's loads below later MFMAs (it otherwise trades the
+    // chunks in flight for registers: vmcnt(8) = two chunks in flight on the down projection)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wb[d][t][s]), xv, acc[t]);
-        }
-        if (j + DEPTH < mine) {
-          loadw(j + DEPTH, wb[d]);
-          loadx(j + DEPTH, xb[d]);
+    for (int j = 0; j < CPW; ++j) {
+      const int d = j % DEPTH;
+#pragma unroll
+      for (int s = 0; s < U; ++s) {
+        const bf16x8 xv = __builtin_bit_cast(bf16x8, xb[d][s]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wb[d][t][s]), xv, acc[t]);
+      }
+      if (j + DEPTH < CPW) {
+        loadw(j + DEPTH, wb[d]);
+        loadx(j + DEPTH, xb[d]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    for (int base = 0; base < mine; base += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        const int j = base + d;
+        if (j < mine) {
+#pragma unroll
+          for (int s = 0; s < U; ++s) {
+            const bf16x8 xv = __builtin_bit_cast(bf16x8, xb[d][s]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = mfma16(__builtin_bit_cast(bf16x8, wb[d][t][s]), xv, acc[t]);
+          }
+          if (j + DEPTH < mine) {
+            loadw(j + DEPTH, wb[d]);
+            loadx(j + DEPTH, xb[d]);
+          }
         }
       }
     }
@@ -1129,9 +1211,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     for (int t = 0; t < NT; ++t) acc[t] *= rs;
   }
   if constexpr (PRO == 4) {
+    // the raw per-tile entries were loaded with clamped indices (no select before the weight stream): mask here
     float ss = 0.f;
+    if (SS16 && M > 2) {
 #pragma unroll
-    for (int k = 0; k < SSL; ++k) ss += ssv[k];
+      for (int k = 0; k < SSL; ++k) ss += g + 4 * k < e.f.ss_n ? ssv[k] : 0.f;
+    } else {
+      const int lpr = M == 1 ? 64 : 32;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ss += lane % lpr + k * lpr < e.f.ss_n ? ssv[k] : 0.f;
+    }
     if (SS16 && M > 2) {
       ss += __shfl_xor(ss, 16, 64);
       ss += __shfl_xor(ss, 32, 64);
@@ -1178,7 +1267,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
       const int n0 = (tile0 + t) * 16 + q;
       if (m < M && n0 < e.N) {
         float* rp = f.fin_resid + (size_t)m * e.N + n0;
-        f32x4 v = *(const f32x4*)rp;
+        f32x4 v = fin_r[t];
         // all (<= 8) slabs in flight at once: clamped addresses + selects, no per-split branch / wait
         const int Z = (int)gridDim.y;
         u32x2 sa[8], sb[8];
@@ -1197,7 +1286,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
         *(f32x4*)rp = v;
         ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
         if (f.fin_x) {
-          const f32x4 w = *(const f32x4*)(f.norm_w + n0);
+          const f32x4 w = fin_w[t];
           u32x2 pk;
           pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
           pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
@@ -1215,7 +1304,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     epi_gelu_mul4(e, m, tile0 * 16, q, acc[0], acc[1]);
   } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t) epi_qkv_rope4(e, m, (tile0 + t) * 16 + q, acc[t]);
+    for (int t = 0; t < NT; ++t) {
+      f32x4 v = acc[t];
+      const int n0 = (tile0 + t) * 16 + q;
+      if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);
+      f32x4 pr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+      epi_qkv_rope4_core(e, m, n0, v, pr, rope_cs[t], rope_sn[t], e.f.slot_base + rope_slot_raw);
+    }
   } else {
 #pragma unroll
     for (int t = 0; t < NT; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t], z);
@@ -1286,6 +1383,22 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
 
 // measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
 // M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
+// one gemv_kernel launch with the chunks-per-wave specialisation when the K split is exact (see gemv_kernel)
+template <int EPI, int NT, int DEPTH, int PRO, bool FRAG>
+static void launch_gemv_cpw(dim3 grid, size_t lds, hipStream_t st, const bf16_t* A, int lda, const bf16_t* W, int ldw,
+                            int K, int ksplit, const EpiArgs& e) {
+  const int nch = K / 64;                              // U = 2: 64-element chunks
+  const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
+  switch (PG_GEMV_CPW ? cpw : 0) {
+    case 4: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 4>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
+    case 8: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 8>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
+    case 16: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 16>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
+    default: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 0>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
+  }
+}
+
+// measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
+// M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
 template <int EPI, int PRO, bool FRAG>
 static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
@@ -1306,19 +1419,14 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   if constexpr (PG_GEMV_QKV_NT1 && EPI == PG_EPI_QKV_ROPE) {
     if (e.M > 4) {
       // batched q|k|v (2560 rows): one tile per workgroup doubles the grid to 160 workgroups
-      dim3 grid(ntiles, ksplit);
-      hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw,
-                         K, e);
+      launch_gemv_cpw<EPI, 1, PG_GEMV_D2, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
       return;
     }
   }
   if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
-    dim3 grid((ntiles + 1) / 2, ksplit);
-    hipLaunchKernelGGL((gemv_kernel<EPI, 2, 2, PG_GEMV_D2, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K,
-                       e);
+    launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(dim3((ntiles + 1) / 2, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   } else {
-    dim3 grid(ntiles, ksplit);
-    hipLaunchKernelGGL((gemv_kernel<EPI, 1, 2, 8, PRO, FRAG>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e);
+    launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   }
 }
 
@@ -1458,7 +1566,7 @@ extern "C" int pg_attn_oproj(const void* q, long q_rs, const void* k, long k_bs,
              fused->q_per_kv == Hq / Hkv && fused->part_o && fused->part_ml);
   AttnArgs a{(const bf16_t*)q, q_rs, nullptr, 0, (const bf16_t*)k, k_bs, k_hs, k_rs, (const bf16_t*)vt, vt_bs, vt_hs,
              vt_ds, nullptr, 0, 0, 1, 1, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys,
-             (float*)fused->part_o, (float*)fused->part_ml};
+             (float*)fused->part_o, (float*)fused->part_ml, 0};
   return gemm_impl(nullptr, K, W, ldw, nullptr, C, ldc, B, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream,
                    &a, B * Hkv * fused->asplit, sync);
 }

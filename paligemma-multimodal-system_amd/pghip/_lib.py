@@ -39,7 +39,7 @@ SIGNATURES = {
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
-                     i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, vp],
+                     i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp],
     "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
     "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],
     "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],

@@ -429,7 +429,8 @@ class PaliGemmaEngine:
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml)
+                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml,
+                          kcap=cache.Smax)
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                 akeys=SK)
@@ -509,7 +510,7 @@ class PaliGemmaEngine:
                               cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                               B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                               scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                              part_ml=part_ml)
+                              part_ml=part_ml, kcap=cache.Smax)
             if not merge_in_gemv:
                 ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
                 fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
@@ -566,7 +567,7 @@ class PaliGemmaEngine:
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=SK or self.DECODE_SPLIT_KEYS, nsplit=nsplit,
-                          part_o=part_o, part_ml=part_ml)
+                          part_o=part_o, part_ml=part_ml, kcap=cache.Smax)
             ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
             self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
             self._allreduce(part[:so])

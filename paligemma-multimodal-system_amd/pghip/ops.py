@@ -206,11 +206,12 @@ def norm_residual_fp8(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, sca
 
 def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lq, Lkv, Hq, Hkv, D,
               scale, mask=None, mask_bs=0, mask_rs=0, lkv_dev=None, split_keys=0, nsplit=0, part_o=None,
-              part_ml=None):
-    """q/k/vt/o are base tensors (bf16) with explicit element strides (see include/pghip.h)."""
+              part_ml=None, kcap=0):
+    """q/k/vt/o are base tensors (bf16) with explicit element strides (see include/pghip.h).  kcap (decode): the
+    static cache's row capacity Smax, so each split's first K/V block is loaded before the kv length arrives."""
     _lib.call("pg_attention", _p(q), q_rs, _p(o), o_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds,
               _p(mask), mask_bs, mask_rs, B, Lq, Lkv, _p(lkv_dev), Hq, Hkv, D, float(scale), split_keys, nsplit,
-              _p(part_o), _p(part_ml), _s())
+              _p(part_o), _p(part_ml), int(kcap), _s())
 
 
 def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):

@@ -265,6 +265,15 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
                   nsplit=nsplit, part_o=po, part_ml=pml)
     ops.attn_combine(po, pml, od, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
     assert err(od, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2
+    # kcap = Smax: every split's first block is loaded before the kv length is read (rows past it masked after
+    # the loads land): bit-identical partials and output
+    if Smax % 32 == 0:
+        po2, pml2, od2 = torch.empty_like(po), torch.empty_like(pml), torch.empty_like(od)
+        ops.attention(qd, nh * hd, od2, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
+                      B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=SK,
+                      nsplit=nsplit, part_o=po2, part_ml=pml2, kcap=Smax)
+        ops.attn_combine(po2, pml2, od2, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+        assert torch.equal(od2, od)
 
 
 def test_rope_kv_write_matches_reference_formula():
