@@ -18,6 +18,7 @@
 //
 // Replaces the nn.Linear call sites of modeling_siglip.py:59-62,177-178,
 // modeling_paligemma.py:57, modeling_gemma.py:205-207,255-259,484.
+#include <cstdlib>
 #include <type_traits>
 
 #include "attn_common.h"
@@ -878,13 +879,20 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         const long base0 = (((long)m * f.kv_heads + hq / G) * S) * 16 + (hq % G);
         float ms[16], ls[16];
         f32x4 o4[16];
+        f32x2 mlv[16];
+        // all 32 loads issued back to back before any is used (sched_barrier): the scheduler otherwise recycled
+        // one register for six of the O loads, a load -> wait -> load chain of six round trips
 #pragma unroll
         for (int sp = 0; sp < 16; ++sp) {
           const long bs = base0 + (long)min(sp, S - 1) * 16;
-          const f32x2 v = PRO == 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
-          ms[sp] = sp < S ? v[0] : -INFINITY;
-          ls[sp] = v[1];
+          mlv[sp] = PRO == 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
           o4[sp] = PRO == 5 ? ld16_wt(f.part_o + bs * f.dtw + d4 * 4) : *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int sp = 0; sp < 16; ++sp) {
+          ms[sp] = sp < S ? mlv[sp][0] : -INFINITY;
+          ls[sp] = mlv[sp][1];
         }
         float mx = ms[0];
 #pragma unroll
@@ -1027,10 +1035,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
   // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
   // own row, so the row total is a reduction over the 4 lane groups
-  // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- run the DEPTH = PG_GEMV_D2 ring and use
-  // the same 16-entry layout as the two-tile form)
-  static_assert(PG_GEMV_D2 != 8, "the one-tile M > 4 GEMV is told apart from the M <= 4 one by its ring depth");
-  constexpr bool SS16 = PRO == 4 && (NT == 2 || DEPTH != 8);
+  // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- use the same 16-entry layout as the
+  // two-tile form)
+  constexpr bool SS16 = PRO == 4 && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
   constexpr int SSL = SS16 ? 16 : 4;
   float ssv[SSL];
 #pragma unroll
@@ -1389,7 +1396,9 @@ static void launch_gemv_cpw(dim3 grid, size_t lds, hipStream_t st, const bf16_t*
                             int K, int ksplit, const EpiArgs& e) {
   const int nch = K / 64;                              // U = 2: 64-element chunks
   const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
-  switch (PG_GEMV_CPW ? cpw : 0) {
+  // PG_GEMV_CPW_OFF=1 (environment, tuning A/B only): the runtime-loop kernel everywhere
+  static const bool cpw_off = getenv("PG_GEMV_CPW_OFF") && atoi(getenv("PG_GEMV_CPW_OFF")) != 0;
+  switch (PG_GEMV_CPW && !cpw_off ? cpw : 0) {
     case 4: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 4>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
     case 8: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 8>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
     case 16: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 16>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
@@ -1423,10 +1432,19 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
       return;
     }
   }
+  // PG_GEMV_D_NT2 / PG_GEMV_D_NT1 (environment, tuning A/B only): ring depth of the two-tile / one-tile kernels
+  static const int d2 = getenv("PG_GEMV_D_NT2") ? atoi(getenv("PG_GEMV_D_NT2")) : PG_GEMV_D2;
+  static const int d1 = getenv("PG_GEMV_D_NT1") ? atoi(getenv("PG_GEMV_D_NT1")) : 8;
   if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
-    launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(dim3((ntiles + 1) / 2, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
+    const dim3 grid((ntiles + 1) / 2, ksplit);
+    if (d2 == 2) launch_gemv_cpw<EPI, 2, 2, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+    else if (d2 == 3) launch_gemv_cpw<EPI, 2, 3, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+    else launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
   } else {
-    launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
+    const dim3 grid(ntiles, ksplit);
+    if (d1 == 4) launch_gemv_cpw<EPI, 1, 4, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+    else if (d1 == 6) launch_gemv_cpw<EPI, 1, 6, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+    else launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
   }
 }
 
