@@ -129,6 +129,21 @@ int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part
                      const float* b, void* out, int ldo, float* out_f32, const int* row_map, int M_out,
                      int H, int mode, float eps, int write_resid, hipStream_t stream);
 
+/* Decode attention block in ONE launch (batch <= 2, head_dim 256, single rank): the q|k|v GEMV (fq: pro 1 or 4,
+ * RoPE + KV append) -> split-KV attention (waves of the same launch; q and the new k / v rows handed over
+ * write-through through pub_k / pub_v [M][Hkv*256] bf16) -> merge + o_proj GEMV + split-K finalisation (fo:
+ * the PG_EPI_F32_FIN and merge fields; akeys = 32, asplit <= 16).  Replaces pg_gemm_fused(q|k|v) + pg_attention
+ * + pg_gemm_fused(o_proj) of a decode layer: gemma.py:264-358 + KVCache.update :18-57.  sync: 4 zeroed ints
+ * (self-resetting; sync[3] = 1 if a wait timed out).  Returns hipErrorNotSupported with nothing launched when
+ * the grid cannot be co-resident on this device (the caller then runs the three launches). */
+int pg_decode_attn_block(const void* xq, const void* wqkv, void* qbuf, const PgFusedArgs* fq, const void* wo,
+                         float* oslab, const PgFusedArgs* fo, int ksplit_o, int M, int H, void* pub_k, void* pub_v,
+                         int* sync, hipStream_t stream);
+
+/* Diagnostics: every later pg_decode_attn_block launch records per workgroup [start, end of its wait, end, -]
+ * (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
+int pg_decode_block_stamps(void* buf);
+
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
  * split-KV partials, merge with pg_attn_combine; kcap > 0 = readable cache rows (Smax, multiple of 32): each split's

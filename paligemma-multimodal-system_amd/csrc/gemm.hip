@@ -117,6 +117,12 @@ struct EpiArgs {
   int att_total;             // B * Hkv * nsplit splits
   int att_wgs;
   int* sync;
+  // decode attention block (pg_decode_attn_block): the q|k|v epilogue publishes for consumers in the same launch --
+  // q stored write-through, the new k / v rows also write-through to pub_k / pub_v [B][Hkv*D]
+  int pub;
+  bf16_t* pub_k;
+  bf16_t* pub_v;
+  unsigned long long* stamps;   // diagnostics (pg_decode_block_stamps): [blockIdx.x][4], [1] = end of the PRO 6 wait
 };
 
 // fp8 dequantisation of one accumulator fragment: C[m][n0..n0+3] *= a_scale[m] * w_scale[n0..n0+3]
@@ -161,15 +167,29 @@ __device__ __forceinline__ void epi_qkv_rope4_core(const EpiArgs& e, int m, int 
     u32x2 pk;
     pk[0] = pack_bf2(y[0], y[1]);
     pk[1] = pack_bf2(y[2], y[3]);
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
     if (blk < Hq) {
-      *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0) = pk;
-    } else if (in_cache) {
-      *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
+      bf16_t* qp = (bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0;
+      if (e.pub) __hip_atomic_store((gu64*)qp, __builtin_bit_cast(unsigned long long, pk), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+      else *(u32x2*)qp = pk;
+    } else {
+      if (in_cache) *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
+      if (e.pub) __hip_atomic_store((gu64*)(e.pub_k + (size_t)b * KV + (blk - Hq) * D + d0),
+                                    __builtin_bit_cast(unsigned long long, pk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  } else if (in_cache) {
+  } else {
     const int c0 = (blk - Hq - Hkv) * D + d0;
+    if (in_cache) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
+      for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
+    }
+    if (e.pub) {
+      typedef __attribute__((address_space(1))) unsigned long long gu64;
+      const u32x2 pv = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+      __hip_atomic_store((gu64*)(e.pub_v + (size_t)b * KV + c0), __builtin_bit_cast(unsigned long long, pv),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -731,6 +751,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_FRAG_NT
 #define PG_GEMV_FRAG_NT 1
 #endif
+#ifndef PG_BLOCK_TIMEOUT_TICKS
+#define PG_BLOCK_TIMEOUT_TICKS 20000000ull    // 0.2 s of the 100 MHz constant clock: a fused-launch wait gives up
+#endif
 #ifndef PG_GEMV_CPW
 #define PG_GEMV_CPW 1     // decode GEMV: straight-line chunk loop when every wave owns the same chunk count
 #endif
@@ -738,9 +761,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #define PG_MERGE_V2 1
 #endif
 
+// the GEMV's workgroup coordinates: blockIdx / gridDim of its own launch, or a role's virtual ones inside a fused
+// launch (decode_block.hip)
+struct GemvIdx {
+  int bx, by, nx, ny;
+};
+
 template <int PRO>
 __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, int k0, int Kr, bf16_t* xs,
-                                              float* scratch, const bf16_t* __restrict__ A, int lda) {
+                                              float* scratch, const bf16_t* __restrict__ A, int lda,
+                                              const GemvIdx& gi) {
   const PgFusedArgs& f = e.f;
   const int t = threadIdx.x;
   const int ldx = Kr + XPAD;
@@ -754,7 +784,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
   } else if constexpr (PRO == 1) {
     // RMSNorm over the FULL row (Kr == K): pass 1 sum of squares, pass 2 normalise into LDS
     const int K4 = K >> 2;
-    const bool w0 = blockIdx.x == 0 && blockIdx.y == 0 && f.resid_out != nullptr;
+    const bool w0 = gi.bx == 0 && gi.by == 0 && f.resid_out != nullptr;
     float* red = scratch;   // [4 waves][16 rows]
     if (M == 1 && K4 <= 4 * 256) {
       // one row: keep it in registers between the two passes (one dependent round trip fewer)
@@ -836,11 +866,28 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
     }
     __syncthreads();
     if (t < M) red[64 + t] = rsqrtf((red[t] + red[16 + t] + red[32 + t] + red[48 + t]) / (float)K + f.eps);
-  } else if constexpr ((PRO == 2 && PG_MERGE_V2) || PRO == 5) {
+  } else if constexpr ((PRO == 2 && PG_MERGE_V2) || PRO == 5 || PRO == 6) {
+    if constexpr (PRO == 6) {
+      // decode attention block (pg_decode_attn_block): the attention waves of the same launch publish their
+      // partials write-through and add to sync[0]; wait for all att_total of them (weights already in flight),
+      // bounded by the wall clock (sync[3] = 1 on a timeout: the outputs are then meaningless)
+      if (t == 0) {
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(e.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.att_total) {
+          if (wall_clock64() - t0 > PG_BLOCK_TIMEOUT_TICKS) {
+            __hip_atomic_store(e.sync + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (e.stamps) e.stamps[blockIdx.x * 4 + 1] = wall_clock64();
+      }
+      __syncthreads();
+    }
     if constexpr (PRO == 5) {
       // attention role (workgroups [0, att_wgs)): 4 splits, one per wave; then publish (drained write-through
       // stores, workgroup barrier, one relaxed agent-scope add).  Every workgroup then waits for all of them.
-      const int wg = blockIdx.y * gridDim.x + blockIdx.x;
+      const int wg = gi.by * gi.nx + gi.bx;
       if (wg < e.att_wgs) {
         const int id = wg * PG_AO_SPLITS_PER_WG + (t >> 6);
         if ((t >> 6) < PG_AO_SPLITS_PER_WG && id < e.att_total) {
@@ -885,8 +932,8 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
 #pragma unroll
         for (int sp = 0; sp < 16; ++sp) {
           const long bs = base0 + (long)min(sp, S - 1) * 16;
-          mlv[sp] = PRO == 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
-          o4[sp] = PRO == 5 ? ld16_wt(f.part_o + bs * f.dtw + d4 * 4) : *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+          mlv[sp] = PRO >= 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
+          o4[sp] = PRO >= 5 ? ld16_wt(f.part_o + bs * f.dtw + d4 * 4) : *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -912,11 +959,13 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
       }
       __syncthreads();
-      if (PRO == 5 && t == 0) {
-        const int total = gridDim.x * gridDim.y;
+      if ((PRO == 5 || PRO == 6) && t == 0) {
+        const int total = gi.nx * gi.ny;
         if (__hip_atomic_fetch_add(e.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
           __hip_atomic_store(e.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);       // every wait is over
           __hip_atomic_store(e.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // PRO 6: also the q|k|v arrival counter (every attention wave passed its wait before adding to sync[0])
+          if (PRO == 6) __hip_atomic_store(e.sync + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       return;
@@ -994,21 +1043,21 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
 // wait only for that chunk (vmcnt(N), N = younger loads), instead of the conservative vmcnt(0) that the runtime
 // loop and its exec-masked loads produce at every ring turn (the ring drained before its first MFMA).
 template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG, int CPW = 0>
-__global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
-                                                   const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
+__device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda, const bf16_t* __restrict__ W,
+                                          int ldw, int K, const EpiArgs& e, const GemvIdx gi) {
   constexpr int CH = U * 32;
   extern __shared__ __attribute__((aligned(16))) char dyn_smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int r = lane & 15;
-  const int tile0 = blockIdx.x * NT;
+  const int tile0 = gi.bx * NT;
   const int M = e.M;
   const bool xvalid = r < M;
 
-  const int z = blockIdx.y;
+  const int z = gi.by;
   const int nch_all = K / CH;
-  const int per_z = (nch_all + gridDim.y - 1) / gridDim.y;
+  const int per_z = (nch_all + gi.ny - 1) / gi.ny;
   const int c0 = z * per_z;
   const int nch = min(nch_all - c0, per_z);
   const int mine = CPW > 0 ? CPW : (nch > wave ? (nch - wave + 3) / 4 : 0);   // chunks wave, wave+4, ...
@@ -1121,7 +1170,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
   // weights issued before the prologue, except by the attention workgroups of pro_mode 5 (their publish
   // drains vmcnt: the attention result, not their weights, is on everyone's critical path)
-  const bool prew = STAGED && PG_GEMV_PREW && !(PRO == 5 && (int)(blockIdx.y * gridDim.x + blockIdx.x) < e.att_wgs);
+  const bool prew = STAGED && PG_GEMV_PREW && !(PRO == 5 && gi.by * gi.nx + gi.bx < e.att_wgs);
   if (prew) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
@@ -1129,7 +1178,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
   }
   if constexpr (STAGED) {
     float* scratch = (float*)(dyn_smem + (((size_t)M * (Kr + XPAD) * 2 + 15) & ~(size_t)15));
-    gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch, A, lda);
+    gemv_prologue<PRO>(e, M, K, c0 * CH, nch * CH, xs, scratch, A, lda, gi);
   }
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
@@ -1248,6 +1297,34 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     // The reducer reads the slabs with sc1 loads (bypass its L1/L2), so no acquire fence either.
     const PgFusedArgs& f = e.f;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
+    auto finish = [&](int t, int n0, f32x4 v, float& ssl) {   // v = the finalised residual of (m, n0..n0+3)
+      *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
+      ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+      if (f.fin_x) {
+        const f32x4 w = fin_w[t];
+        u32x2 pk;
+        pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
+        pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
+        *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
+      }
+    };
+    if (gi.ny == 1) {
+      // no split: this workgroup owns the tile -- no slab, no ticket (same sums: residual + (acc + bias))
+      float ssl = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n0 = (tile0 + t) * 16 + q;
+        if (m < M && n0 < e.N) {
+          f32x4 v = acc[t];
+          if (e.bias) v += load4_guard(e.bias, n0, e.N);
+          finish(t, n0, fin_r[t] + v, ssl);
+        }
+      }
+      ssl += __shfl_xor(ssl, 16, 64);
+      ssl += __shfl_xor(ssl, 32, 64);
+      if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = (tile0 + t) * 16 + q;
@@ -1264,19 +1341,18 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (PG_T_NOFIN) return;                                  // timing experiment only: slabs never reduced
     int old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(f.fin_cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) old = __hip_atomic_fetch_add(f.fin_cnt + gi.bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0, 64);
-    if (old != (int)gridDim.y - 1) return;
+    if (old != gi.ny - 1) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep the loads below the ticket
     float ssl = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = (tile0 + t) * 16 + q;
       if (m < M && n0 < e.N) {
-        float* rp = f.fin_resid + (size_t)m * e.N + n0;
         f32x4 v = fin_r[t];
         // all (<= 8) slabs in flight at once: clamped addresses + selects, no per-split branch / wait
-        const int Z = (int)gridDim.y;
+        const int Z = gi.ny;
         u32x2 sa[8], sb[8];
 #pragma unroll
         for (int zz = 0; zz < 8; ++zz) {
@@ -1290,21 +1366,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
                             __uint_as_float(sb[zz][1])};
           v += zz < Z ? sv : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        *(f32x4*)rp = v;
-        ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-        if (f.fin_x) {
-          const f32x4 w = fin_w[t];
-          u32x2 pk;
-          pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
-          pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
-          *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
-        }
+        finish(t, n0, v, ssl);
       }
     }
     ssl += __shfl_xor(ssl, 16, 64);
     ssl += __shfl_xor(ssl, 32, 64);
-    if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + blockIdx.x] = ssl;
-    if (lane == 0) __hip_atomic_store(f.fin_cnt + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
+    if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
@@ -1324,6 +1392,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 #pragma unroll
     for (int t = 0; t < NT; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t], z);
   }
+}
+
+template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG, int CPW = 0>
+__global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
+                                                   const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
+  gemv_body<EPI, NT, U, DEPTH, PRO, FRAG, CPW>(A, lda, W, ldw, K, e,
+                                               GemvIdx{(int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y});
 }
 
 // --------------------------------------------------------------------------------------
@@ -1622,4 +1697,156 @@ extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc,
 extern "C" int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
                              int M, int N, int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream) {
   return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream);
+}
+
+// --------------------------------------------------------------------------------------
+// Decode attention block: q|k|v GEMV (RMSNorm prologue, RoPE + KV append) -> split-KV attention -> merge + o_proj
+// GEMV + in-kernel split-K finalisation, as ONE launch (batch <= 2, head_dim 256).  Replaces the three launches of
+// GemmaAttention.forward's decode step (modeling_gemma.py:264-358).  Roles by workgroup index: [0, nq) the q|k|v
+// tile pairs, [nq, nq + na) the attention (4 splits per workgroup, one per wave), then the o_proj (tile, split)
+// workgroups.  A role waits only for lower roles, and the launch is refused unless the whole grid is co-resident
+// (occupancy x CUs; the attention role's registers make it one 256-thread workgroup per CU, so the grid is sized
+// to at most one per CU: q|k|v as tile pairs, o_proj unsplit), so no wait depends on a workgroup that has not been
+// dispatched.  Hand-offs (MI355X guide, inter-workgroup hand-off table row 1): producers store write-through,
+// drain vmcnt, then one relaxed agent-scope add per workgroup (q|k|v: sync[2]) or per wave (attention: sync[0]);
+// consumers poll with relaxed agent loads and read the handed-off bytes with write-through-readable loads.
+// What the launch buys: the attention issues its cached K/V block and the o_proj its weights while the q|k|v
+// GEMV still streams, and two kernel boundaries go.
+struct DecodeBlockArgs {
+  const bf16_t* xq;      // q|k|v input x' (pro 4) or null (pro 1: RMSNorm of the residual)
+  int lda;
+  const bf16_t* wqkv;
+  EpiArgs eq;            // q|k|v epilogue, pub = 1
+  AttnArgs att;          // FUSED decode splits
+  const bf16_t* wo;
+  EpiArgs eo;            // o_proj: pro 6, PG_EPI_F32_FIN
+  int K, Ko;             // q|k|v input width (hidden), o_proj input width (q heads x head_dim)
+  int nq, na, no_tiles, ko;
+  int* sync;             // [0] attention waves done, [1] o workgroups past the merge, [2] q|k|v tiles done, [3] err
+  unsigned long long* stamps;   // diagnostics only (pg_decode_block_stamps): [workgroup][4] wall-clock stamps
+};
+
+static unsigned long long* g_block_stamps = nullptr;
+// Diagnostics: record per workgroup of every later pg_decode_attn_block launch its start, the end of its wait
+// (or of its GEMV main loop), and its end (100 MHz wall clock) into buf [grid][4] u64; null turns it off.
+extern "C" int pg_decode_block_stamps(void* buf) {
+  g_block_stamps = (unsigned long long*)buf;
+  return 0;
+}
+
+template <int PROQ, int CQ, int CO>
+__global__ __launch_bounds__(256) void decode_attn_block_kernel(DecodeBlockArgs a) {
+  int bid = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned long long* stamp = a.stamps ? a.stamps + (size_t)blockIdx.x * 4 : nullptr;
+  if (stamp && threadIdx.x == 0) stamp[0] = wall_clock64();
+  if (bid < a.nq) {
+    gemv_body<PG_EPI_QKV_ROPE, 2, 2, PG_GEMV_D2, PROQ, true, CQ>(a.xq, a.lda, a.wqkv, a.K, a.K, a.eq,
+                                                                  GemvIdx{bid, 0, a.nq, 1});
+    if (wave == 0) {   // wave 0 stored the tile write-through: drain, then arrive
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(a.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stamp && lane == 0) stamp[2] = wall_clock64();
+    }
+    return;
+  }
+  bid -= a.nq;
+  if (bid < a.na) {
+    const int id = bid * 4 + wave;
+    if (id >= a.eo.att_total) return;
+    const int ns = a.eo.f.asplit;
+    const int sp = id % ns, kvh = (id / ns) % a.att.Hkv, b = id / (ns * a.att.Hkv);
+    attn_decode_split<256, 16, true, true, true>(a.att, b, kvh, sp, ns, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stamp && threadIdx.x == 0) stamp[2] = wall_clock64();
+    return;
+  }
+  bid -= a.na;
+  gemv_body<PG_EPI_F32_FIN, 1, 2, 8, 6, true, CO>(nullptr, a.Ko, a.wo, a.Ko, a.Ko, a.eo,
+                                                  GemvIdx{bid % a.no_tiles, bid / a.no_tiles, a.no_tiles, a.ko});
+  if (stamp && threadIdx.x == 0) stamp[2] = wall_clock64();
+}
+
+template <int PROQ, int CQ, int CO>
+static int launch_decode_block(const DecodeBlockArgs& a, size_t lds, hipStream_t stream) {
+  // workgroups that can be resident at once: occupancy x CUs.  The occupancy API can answer one workgroup per CU
+  // too many when SGPRs bind (MI355X guide: residency), which only happens above two per CU: keep a margin there.
+  static int cap = -1;
+  if (cap < 0) {
+    int nb = 0, dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_attn_block_kernel<PROQ, CQ, CO>, 256, 8192) !=
+            hipSuccess)
+      return (int)hipErrorNotSupported;
+    cap = (nb <= 2 ? nb : nb - 1) * cus;
+  }
+  const int grid = a.nq + a.na + a.no_tiles * a.ko;
+  if (grid > cap) return (int)hipErrorNotSupported;     // the caller runs the three-launch form instead
+  hipLaunchKernelGGL((decode_attn_block_kernel<PROQ, CQ, CO>), dim3(grid), dim3(256), lds, stream, a);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
+// fq: the q|k|v GEMV's fused args (pro 1 or 4, RoPE / KV-cache fields; slot_dev = kv length before this token);
+// fo: the o_proj's (F32_FIN fields + the split-KV merge fields: part_o / part_ml / asplit <= 16 / akeys = keys per
+// split).  sync: 4 zeroed ints owned by the caller (self-resetting; sync[3] = 1 after a timed-out wait).
+// pub_k / pub_v: [M][Hkv * head_dim] bf16 scratch.  Returns hipErrorNotSupported (nothing launched) when the
+// grid cannot be co-resident on this device.
+extern "C" int pg_decode_attn_block(const void* xq, const void* wqkv, void* qbuf, const PgFusedArgs* fq,
+                                    const void* wo, float* oslab, const PgFusedArgs* fo, int ksplit_o, int M, int H,
+                                    void* pub_k, void* pub_v, int* sync, hipStream_t stream) {
+  PG_REQUIRE(fq && fo && wqkv && qbuf && wo && oslab && pub_k && pub_v && sync && M >= 1 && M <= 2);
+  PG_REQUIRE((fq->pro_mode == 1 && xq == nullptr && fq->resid_in && fq->norm_w && fq->nsplit == 0) ||
+             (fq->pro_mode == 4 && xq != nullptr && fq->ss_in && fq->ss_n > 0 && fq->ss_ld >= fq->ss_n &&
+              fq->ss_n <= 256 && (M == 1 || fq->ss_n <= 128)));
+  const int D = fq->head_dim, Hq = fq->q_heads, Hkv = fq->kv_heads;
+  PG_REQUIRE(D == 256 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && fq->cos_t && fq->sin_t && fq->pos &&
+             fq->kc && fq->vtc && fq->slot_dev && fq->rows_per_batch == 1 && fq->smax >= 32 && fq->smax % 32 == 0);
+  const int Nq = (Hq + 2 * Hkv) * D, Ko = Hq * D;
+  PG_REQUIRE(H % 256 == 0 && Ko % (256 * ksplit_o) == 0 && ksplit_o >= 1 && ksplit_o <= 8);
+  PG_REQUIRE(fo->fin_cnt && fo->fin_resid && fo->ss_out && fo->ss_ld >= H / 16 && fo->part_o && fo->part_ml &&
+             fo->asplit > 0 && fo->asplit <= 16 && fo->asplit % 4 == 0 && fo->head_dim == D && fo->kv_heads == Hkv &&
+             fo->q_per_kv == Hq / Hkv && fo->akeys == 32 && fo->asplit * 32 >= fq->smax &&
+             (fo->fin_x == nullptr || fo->norm_w != nullptr));
+  DecodeBlockArgs a{};
+  a.xq = (const bf16_t*)xq;
+  a.lda = H;
+  a.wqkv = (const bf16_t*)wqkv;
+  a.eq = EpiArgs{nullptr, qbuf, Ko, M, Nq, nullptr, 0, nullptr, 0, 0, *fq};
+  a.eq.pub = 1;
+  a.eq.pub_k = (bf16_t*)pub_k;
+  a.eq.pub_v = (bf16_t*)pub_v;
+  const int KV = Hkv * D, S = fq->smax;
+  a.att = AttnArgs{(const bf16_t*)qbuf, Ko, nullptr, 0, fq->kc, (long)S * KV, D, KV, fq->vtc, (long)KV * S, (long)D * S,
+                   S, nullptr, 0, 0, 1, 1, Hq / Hkv, Hkv, D, fq->slot_dev,
+                   (1.0f / sqrtf((float)D)) * 1.4426950408889634f, 32, (float*)fo->part_o, (float*)fo->part_ml, S,
+                   sync + 2, 0, (const bf16_t*)pub_k, (const bf16_t*)pub_v, sync + 3};
+  a.wo = (const bf16_t*)wo;
+  PgFusedArgs f6 = *fo;
+  f6.pro_mode = 6;
+  a.eo = EpiArgs{nullptr, oslab, H, M, H, nullptr, 0, nullptr, 0, 0, f6};
+  a.eo.att_total = M * Hkv * fo->asplit;
+  a.eo.sync = sync;
+  a.K = H;
+  a.Ko = Ko;
+  PG_REQUIRE(Nq % 32 == 0);
+  a.nq = Nq / 32;                                  // tile pairs
+  a.na = (a.eo.att_total + 3) / 4;
+  a.no_tiles = H / 16;
+  a.ko = ksplit_o;
+  a.att.wait_target = a.nq;
+  a.sync = sync;
+  a.stamps = g_block_stamps;
+  a.eo.stamps = g_block_stamps;
+  a.att.stamps = g_block_stamps;
+  // o_proj x staged in LDS by the merge prologue: M rows of this split's K range
+  const size_t lds = (((size_t)M * (Ko / ksplit_o + XPAD) * 2 + 15) & ~(size_t)15) + 64 * sizeof(float);
+  const int cq = H / 256, co = Ko / ksplit_o / 256;
+  if (fq->pro_mode == 4 && cq == 8 && co == 4) return launch_decode_block<4, 8, 4>(a, lds, stream);
+  if (fq->pro_mode == 1 && cq == 8 && co == 4) return launch_decode_block<1, 8, 4>(a, lds, stream);
+  if (fq->pro_mode == 4 && cq == 8 && co == 8) return launch_decode_block<4, 8, 8>(a, lds, stream);
+  if (fq->pro_mode == 1 && cq == 8 && co == 8) return launch_decode_block<1, 8, 8>(a, lds, stream);
+  return (int)hipErrorNotSupported;
 }

@@ -63,7 +63,8 @@ class KVStore:
 
 
 class PaliGemmaEngine:
-    DECODE_SPLIT_O = 2      # split-K of o_proj at decode (partials reduced by the next RMSNorm)
+    DECODE_SPLIT_O = 1      # split-K of o_proj at decode: unsplit, the GEMV finalises its own tile (no slab, no ticket;
+                            # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
@@ -81,6 +82,12 @@ class PaliGemmaEngine:
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
     FUSE_ATTN_O = False     # with USE_FIN: the split-KV attention inside the o_proj launch (pg_attn_oproj): correct,
                             # measured 1.31 vs 1.19 ms/token (the fused GEMV drops to 1 wave/SIMD; 252 pollers)
+    # with USE_FIN, B <= FUSE_MAX_B: q|k|v + attention + o_proj of a layer as ONE launch (pg_decode_attn_block)
+    # correct (bit-exact vs the three launches) but measured slower: 28.2 vs 16.5 us per layer on MI355X -- the
+    # in-launch hand-offs (2.7 us q|k|v -> attention, ~1 us attention -> o_proj) cost more than the two kernel
+    # boundaries they remove, so it is off
+    FUSE_BLOCK = os.environ.get("PG_FUSE_BLOCK", "0") == "1"
+    BLOCK_SPLIT_O = int(os.environ.get("PG_BLOCK_SPLIT_O", "1"))   # o_proj split-K inside the block launch
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -91,6 +98,8 @@ class PaliGemmaEngine:
         if self.comm.world != self.tp:
             raise ValueError(f"weights packed for tp_world={self.tp}, communicator has world {self.comm.world}")
         self.split_o = self.DECODE_SPLIT_O if self.tp == 1 else 1        # smaller all-reduce messages under TP
+        if os.environ.get("PG_SPLIT_O"):                                   # tuning override
+            self.split_o = int(os.environ["PG_SPLIT_O"])
         self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         self.device = torch.device(device)
         self.image_token_id = cfg.get("image_token_index", 256000)
@@ -101,6 +110,7 @@ class PaliGemmaEngine:
         self._rope_n = 0
         self._ws = {}
         self.graphs = {}
+        self._block_ok = True      # pg_decode_attn_block accepted by this device (else the three-launch form)
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name, shape, dtype):
@@ -460,6 +470,12 @@ class PaliGemmaEngine:
             self.sample(logits, st, sampler, advance=True)
         return logits
 
+    def check(self):
+        """Raise if a fused decode launch gave up waiting inside the launch (its outputs are then invalid)."""
+        sync = self._ws.get("d_block_sync")
+        if sync is not None and int(sync[3].item()):
+            raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
+
     def _zeros(self, name, shape, dtype):
         """Persistent zero-initialised buffer (e.g. self-resetting arrival tickets)."""
         t = self._ws.get(name)
@@ -493,10 +509,40 @@ class PaliGemmaEngine:
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
         SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
+        block = (self.FUSE_BLOCK and merge_in_gemv and self._block_ok and w.frag and hd == 256 and SK == 32 and
+                 nsplit <= 16 and cache.Smax % 32 == 0)
+        if block:
+            pub_k = self._buf("d_pub_k", (B, kvd), torch.bfloat16)
+            pub_v = self._buf("d_pub_v", (B, kvd), torch.bfloat16)
+            sync = self._zeros("d_block_sync", (4,), torch.int32)
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                         q_heads=nh, kv_heads=nkv)
+            if block:
+                # q|k|v + attention + o_proj in one launch (pg_decode_attn_block)
+                if i == 0:
+                    fq = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
+                                        **rope)
+                else:
+                    fq = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
+                fo = ops.fused_args(part_o=part_o, part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt,
+                                    q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt,
+                                    fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
+                ok = ops.decode_attn_block(None if i == 0 else xq, Lw["qkv_w"], qb, fq, Lw["o_w"], part, fo,
+                                           ksplit_o=self.BLOCK_SPLIT_O, M=B, pub_k=pub_k, pub_v=pub_v, sync=sync)
+                if not ok:
+                    if i > 0:
+                        raise RuntimeError("pg_decode_attn_block refused a later layer of the same step")
+                    self._block_ok = False      # this device cannot hold the grid: the three launches from now on
+                    block = False
+                else:
+                    nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
+                    fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
+                    ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+                    fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+                    ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
+                    continue
             if i == 0:      # the embedding rows are final: plain RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                     **rope)
@@ -648,6 +694,7 @@ class PaliGemmaEngine:
             step_fn()
             n += 1
         hist = st["hist"][:n].t().contiguous().cpu()
+        self.check()
         if hasattr(self.comm, "check"):
             self.comm.check()              # an xGMI exchange that timed out leaves meaningless sums: raise
         if stop_token is None:

@@ -163,6 +163,25 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
     return out
 
 
+HIP_ERROR_NOT_SUPPORTED = 801
+
+
+def decode_attn_block(xq, Wqkv, qbuf, fq, Wo, oslab, fo, *, ksplit_o: int, M: int, pub_k, pub_v, sync) -> bool:
+    """pg_decode_attn_block: a decode layer's q|k|v GEMV + split-KV attention + o_proj in one launch.  Returns False
+    (nothing launched) when the device cannot hold the whole grid at once; raises on any other error."""
+    _chk(Wqkv, torch.bfloat16, "Wqkv")
+    _chk(Wo, torch.bfloat16, "Wo")
+    _chk(sync, torch.int32, "sync")
+    rc = _lib.load().pg_decode_attn_block(_p(xq), _p(Wqkv), _p(qbuf), _lib.C.byref(fq), _p(Wo), _p(oslab),
+                                          _lib.C.byref(fo), ksplit_o, M, Wqkv.shape[1], _p(pub_k), _p(pub_v),
+                                          _p(sync), _s())
+    if rc == HIP_ERROR_NOT_SUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.PgHipError(f"pg_decode_attn_block failed: hip error {rc} ({_lib._err_string(rc)})")
+    return True
+
+
 def attn_oproj(q, q_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, W, out, fa, sync, *, B, lkv_dev, Hq, Hkv, D,
                scale, split_keys, epi, ksplit, N=None, ldc=None):
     """pg_attn_oproj: split-KV decode attention computed inside the o_proj GEMV launch (fa.pro_mode = 5)."""

@@ -55,6 +55,8 @@ res["down_s8_us"] = timed(lambda i: ops.gemm(hx, L[i % 18]["down_w"], part8, epi
 res["o_s2_us"] = timed(lambda i: ops.gemm(x, L[i % 18]["o_w"], part[:2], epi=ops.EPI_F32 | w.wflag, ksplit=2), 36)
 res["qkv_us"] = timed(lambda i: ops.gemm(x, L[i % 18]["qkv_w"], h[:, :w.qkv_n], epi=ops.EPI_BF16 | w.wflag), 36)
 res["lm_head_us"] = timed(lambda i: ops.gemm(x, w.lm_w, logits, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias), 4)
+res["gateup_same_layer_us"] = timed(lambda i: ops.gemm(x, L[0]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag), 36)
+res["down_same_layer_us"] = timed(lambda i: ops.gemm(hx, L[0]["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=4), 36)
 res["gateup_GBs"] = L[0]["gu_w"].numel() * 2 / res["gateup_us"] / 1e3
 res["down_GBs"] = L[0]["down_w"].numel() * 2 / res["down_s4_us"] / 1e3
 res["lm_head_GBs"] = w.lm_w.numel() * 2 / res["lm_head_us"] / 1e3

@@ -303,3 +303,35 @@ def test_tiny_batched_decode_fin_path_vs_oracle(tiny, golden, B):
         finally:
             eng.USE_FIN = type(eng).USE_FIN
     assert err(outs[True].cpu().numpy(), outs[False].cpu().numpy()) < 5e-3
+
+
+@pytest.mark.slow
+def test_pt224_fused_decode_block_bit_exact(golden):
+    """pg_decode_attn_block (a layer's q|k|v GEMV + split-KV attention + o_proj as ONE launch, q and the new k / v
+    handed over write-through inside the launch) against the three launches with the same o_proj split (1):
+    bit-identical logits, tokens and KV cache over 12 decode steps at full size (head_dim 256), no timed-out
+    wait, every in-launch counter back at zero; then the graph-replayed fused step reproduces the same tokens."""
+    from pghip import configs, engine, synthetic, weights
+    g = golden("pt224")
+    cfg = configs.PT_224
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+    ids = torch.from_numpy(g["input_ids"]).cuda()
+    px = torch.from_numpy(g["pixel_values"]).cuda()
+    runs = []
+    for fused in (True, False):
+        eng.FUSE_BLOCK, eng.split_o = fused, 1
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
+        st = eng.decode_state(1, cache, nxt, 16)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
+        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
+    assert eng._block_ok
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
+    sync = eng._ws["d_block_sync"]
+    assert int(sync[3]) == 0 and int(sync[:3].abs().sum()) == 0
+    eng.FUSE_BLOCK, eng.split_o = type(eng).FUSE_BLOCK, type(eng).DECODE_SPLIT_O
+    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
+    assert out[0].tolist() == runs[0][0]
+    assert int(g["greedy_ids"][0]) == runs[0][0][0]
