@@ -140,6 +140,133 @@ def cpu_baseline(cfg, ids, px, budget_tokens=24):
                       f"{len(out) - 1} decode steps re-running SigLIP like the reference), fp32 numpy, {dt:.1f} s"}
 
 
+class Runner:
+    """One request of the bench workload on an engine: prefill (vision + merge + Gemma prefill, first token
+    sampled) into a static cache, then T-1 decode steps replayed from one captured hipGraph (eager steps when
+    the collectives cannot be captured)."""
+
+    def __init__(self, eng, ids, px, T, sampler, graph_prefill=False, rank=0):
+        B, L = ids.shape
+        self.state = state = {}
+        mask = torch.ones_like(ids)
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, mask, T)
+        st = eng.decode_state(B, cache, nxt, T)
+        eng.sample(logits, st, sampler, advance=False)
+        state.update(cache=cache, feats=feats, st=st)
+        try:
+            if not eng.comm.capturable:
+                raise RuntimeError(f"{eng.comm.backend} collectives are not graph-capturable")
+            self.replay = eng._graph_step(st, cache, feats, sampler)
+            self.graph_mode = "hipgraph"
+        except Exception as e:  # collectives that cannot be captured: eager decode steps
+            log(f"[bench] rank {rank}: decode-step capture failed ({e}); running eager steps")
+            torch.cuda.synchronize()
+            self.replay = lambda: eng.decode_step(state["st"], state["cache"], state["feats"], sampler)  # noqa
+            self.graph_mode = "eager"
+        rows = eng._buf("p_rows", (B,), torch.int32)
+        rows.copy_(torch.arange(B, dtype=torch.int32) * L + (L - 1))
+        pos_pf = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
+
+        def prefill():
+            # vision + merge + Gemma prefill into the decode graph's static cache / state, first token sampled
+            f = eng.vision(px)
+            resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
+            eng.embed_merge(ids, f, resid)
+            lg, _ = eng.gemma_prefill(resid, pos_pf, cache, B, L, logits_rows=rows)
+            state["st"]["pos"].fill_(L + 1)
+            state["st"]["kv_len"].fill_(L)
+            state["st"]["step"].zero_()
+            state["feats"].copy_(f)
+            eng.sample(lg, state["st"], sampler, advance=False)
+
+        # optionally the prefill's ~400 launches as one hipGraph (fixed request shape, as a serving replica would
+        # hold one per shape bucket); measured slower than eager launches on MI355X (pt-224 6.0 vs 5.76 ms,
+        # pt-448 x16 91.6 vs 89.0 ms), so eager is the default
+        self.prefill_run, self.prefill_mode = prefill, "eager"
+        if self.graph_mode == "hipgraph" and graph_prefill:
+            try:
+                prefill()                                  # every workspace allocated outside capture
+                torch.cuda.synchronize()
+                g_pf = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_pf):
+                    prefill()
+                torch.cuda.synchronize()
+                self.prefill_run, self.prefill_mode = g_pf.replay, "hipgraph"
+            except Exception as e:
+                log(f"[bench] rank {rank}: prefill capture failed ({e}); eager prefill")
+                torch.cuda.synchronize()
+        self.T, self.L = T, L
+
+    def request(self):
+        self.prefill_run()
+        for _ in range(self.T - 1):
+            self.replay()
+
+
+def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
+    """The Gemma decoder tensor-parallel over every rank (q heads, gate/up columns and the
+    vocabulary split; decode-size all-reduces as pg_allreduce_xgmi one-shot peer stores over xGMI, larger ones on
+    RCCL): ONE batch-1 request of the same workload across all `world` GPUs (strong scaling of per-token
+    latency).  Reported beside the data-parallel `value`; any failure is reported, never raised."""
+    from pghip import engine, weights
+    from pghip.tp import XgmiComm
+    out = {"tp": world, "comm": "pg_allreduce_xgmi (decode) + RCCL (beyond its buffer)", "scaling": "strong",
+           "workload": "the same request (batch 1) split over all GPUs"}
+    comm = None
+    try:
+        comm = XgmiComm()
+        # sanity exchange before any timed work: rank-dependent values summed exactly, no timeout, on every rank
+        t = torch.full((4096,), float(rank + 1), device="cuda")
+        comm.all_reduce(t)
+        torch.cuda.synchronize()
+        ok = int(comm.err.item()) == 0 and bool((t == world * (world + 1) / 2).all())
+        okt = torch.tensor([1 if ok else 0], device="cuda")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        if not int(okt.item()):
+            raise RuntimeError("xGMI sanity all-reduce failed on some rank")
+        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
+                                     comm=comm)
+        run = Runner(eng, ids[:1], px[:1], T, dict(do_sample=False), False, rank)
+
+        def barrier():
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+        run.request()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run.request()
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], device="cuda")
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        run.prefill_run()
+        ev[1].record()
+        torch.cuda.synchronize()
+        pf_ms = ev[0].elapsed_time(ev[1])
+        ev[0].record()
+        for _ in range(T - 1):
+            run.replay()
+        ev[1].record()
+        torch.cuda.synchronize()
+        dec = ev[0].elapsed_time(ev[1]) / (T - 1)
+        comm.check()
+        out.update(tokens_per_s=round(T * steps / el.item(), 2), ms_per_request=round(el.item() / steps * 1e3, 3),
+                   prefill_ms=round(pf_ms, 3), decode_ms_per_token=round(dec, 4), decode=run.graph_mode)
+        del run, eng
+    except Exception as e:  # reported in the JSON line, the data-parallel measurement stands
+        out["error"] = f"{type(e).__name__}: {e}"[:300]
+    if comm is not None:
+        try:
+            comm.close()
+        except Exception:
+            pass
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,6 +285,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph-prefill", action="store_true",
                     help="replay the prefill as one hipGraph (measured 0.96-0.97x of eager launches: off by default)")
+    ap.add_argument("--no-tp-curve", action="store_true",
+                    help="with --gpus N > 1 and --parallel dp: skip the extra tensor-parallel run of one request over "
+                    "all N GPUs (reported as \"tp\" beside the data-parallel value)")
     ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
                     "instead of greedy, as BASELINE configs[3]")
     args = ap.parse_args()
@@ -201,72 +331,15 @@ def main():
     L = ids.shape[1]
 
     # one request = prefill + T-1 graph-replayed decode steps (first token comes from the prefill)
-    state = {}
     if args.sample:
         g = torch.Generator().manual_seed(4321)
         sampler = dict(do_sample=True, temperature=0.8, top_p=0.9,
                        uniforms=torch.rand(T + 1, B, generator=g).cuda())
     else:
         sampler = dict(do_sample=False)
-
-    def setup():
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, mask, T)
-        st = eng.decode_state(B, cache, nxt, T)
-        eng.sample(logits, st, sampler, advance=False)
-        state.update(cache=cache, feats=feats, st=st)
-        return st
-
-    st = setup()
-    try:
-        if not eng.comm.capturable:
-            raise RuntimeError(f"{eng.comm.backend} collectives are not graph-capturable")
-        replay = eng._graph_step(st, state["cache"], state["feats"], sampler)
-    except Exception as e:  # collectives that cannot be captured: eager decode steps
-        log(f"[bench] rank {rank}: decode-step capture failed ({e}); running eager steps")
-        torch.cuda.synchronize()
-        replay = lambda: eng.decode_step(state["st"], state["cache"], state["feats"], sampler)  # noqa
-        graph_mode = "eager"
-    else:
-        graph_mode = "hipgraph"
-    graph_cache = state["cache"]
-
-    rows = eng._buf("p_rows", (B,), torch.int32)
-    rows.copy_(torch.arange(B, dtype=torch.int32) * L + (L - 1))
-    pos_pf = torch.arange(1, L + 1, device="cuda", dtype=torch.int32).repeat(B, 1)
-
-    def prefill():
-        # vision + merge + Gemma prefill into the decode graph's static cache / state, first token sampled
-        feats = eng.vision(px)
-        resid = eng._buf("p_resid", (B * L, eng.w.hidden), torch.float32)
-        eng.embed_merge(ids, feats, resid)
-        logits, _ = eng.gemma_prefill(resid, pos_pf, graph_cache, B, L, logits_rows=rows)
-        state["st"]["pos"].fill_(L + 1)
-        state["st"]["kv_len"].fill_(L)
-        state["st"]["step"].zero_()
-        state["feats"].copy_(feats)
-        eng.sample(logits, state["st"], sampler, advance=False)
-
-    # optionally the prefill's ~400 launches as one hipGraph (fixed request shape, as a serving replica would
-    # hold one per shape bucket); measured slower than eager launches on MI355X (pt-224 6.0 vs 5.76 ms,
-    # pt-448 x16 91.6 vs 89.0 ms), so eager is the default
-    prefill_run, prefill_mode = prefill, "eager"
-    if graph_mode == "hipgraph" and args.graph_prefill:
-        try:
-            prefill()                                  # every workspace allocated outside capture
-            torch.cuda.synchronize()
-            g_pf = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_pf):
-                prefill()
-            torch.cuda.synchronize()
-            prefill_run, prefill_mode = g_pf.replay, "hipgraph"
-        except Exception as e:
-            log(f"[bench] rank {rank}: prefill capture failed ({e}); eager prefill")
-            torch.cuda.synchronize()
-
-    def request():
-        prefill_run()
-        for _ in range(T - 1):
-            replay()
+    run = Runner(eng, ids, px, T, sampler, args.graph_prefill, rank)
+    request, prefill_run, replay, state = run.request, run.prefill_run, run.replay, run.state
+    graph_mode, prefill_mode = run.graph_mode, run.prefill_mode
 
     def barrier():
         torch.cuda.synchronize()
@@ -320,9 +393,13 @@ def main():
     kern_desc = f"gemv_kernel<GELU_MUL,2> (decode gate/up, 2x{eng.w.inter}x{eng.w.hidden} bf16)"
 
     comm_used = eng.comm
+    eng.check()                                # a fused-launch wait that gave up invalidates the run
+    tp_rec = None
+    if world > 1 and tp == 1 and not args.no_tp_curve:
+        tp_rec = tp_curve(cfg, sd, ids, px, T, rank, world, dist)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        del state, eng
+        del state, eng, run, request, prefill_run, replay
         torch.cuda.empty_cache()
         try:
             cpu = cpu_baseline(cfg, ids_cpu, px_cpu)
@@ -361,6 +438,8 @@ def main():
                          "kernel_avg_us": round(kern_s * 1e6, 2), "bytes_per_launch": kern_bytes},
             "cpu_baseline": cpu,
         }
+        if tp_rec is not None:
+            rec["tp"] = tp_rec
         print(json.dumps(rec), flush=True)
     if hasattr(comm_used, "check"):
         comm_used.check()                      # a timed-out exchange invalidates the run

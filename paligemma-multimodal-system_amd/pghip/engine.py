@@ -63,8 +63,9 @@ class KVStore:
 
 
 class PaliGemmaEngine:
-    DECODE_SPLIT_O = 1      # split-K of o_proj at decode: unsplit, the GEMV finalises its own tile (no slab, no ticket;
-                            # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
+    DECODE_SPLIT_O = 2      # split-K of o_proj at decode (B > FUSE_MAX_B: more workgroups for the batched GEMV)
+    DECODE_SPLIT_O_SMALL = 1  # ... at B <= FUSE_MAX_B: unsplit, the GEMV finalises its own tile (no slab, no ticket;
+                              # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
     DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
@@ -98,8 +99,10 @@ class PaliGemmaEngine:
         if self.comm.world != self.tp:
             raise ValueError(f"weights packed for tp_world={self.tp}, communicator has world {self.comm.world}")
         self.split_o = self.DECODE_SPLIT_O if self.tp == 1 else 1        # smaller all-reduce messages under TP
-        if os.environ.get("PG_SPLIT_O"):                                   # tuning override
+        if os.environ.get("PG_SPLIT_O"):                                   # tuning overrides
             self.split_o = int(os.environ["PG_SPLIT_O"])
+        if os.environ.get("PG_SPLIT_DOWN"):
+            self.split_down = int(os.environ["PG_SPLIT_DOWN"])
         self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         self.device = torch.device(device)
         self.image_token_id = cfg.get("image_token_index", 256000)
@@ -403,7 +406,7 @@ class PaliGemmaEngine:
         xn = self._buf("d_xn", (B, H), torch.bfloat16)
         qb = self._buf("d_q", (B, nh * hd), torch.bfloat16)
         h = self._buf("d_h", (B, I), torch.bfloat16)
-        so, sd = self.split_o, self.split_down
+        so, sd = self._split_o(B), self.split_down
         part = self._buf("d_part", (max(so, sd), B, H), torch.float32)
         SK = self._split_keys(B, cache.Smax)
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
@@ -476,6 +479,11 @@ class PaliGemmaEngine:
         if sync is not None and int(sync[3].item()):
             raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
 
+    def _split_o(self, B: int) -> int:
+        if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
+            return self.DECODE_SPLIT_O_SMALL
+        return self.split_o
+
     def _zeros(self, name, shape, dtype):
         """Persistent zero-initialised buffer (e.g. self-resetting arrival tickets)."""
         t = self._ws.get(name)
@@ -498,7 +506,7 @@ class PaliGemmaEngine:
         B = st["ids"].numel()
         H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
-        so, sd = self.split_o, self.split_down
+        so, sd = self._split_o(B), self.split_down
         tiles = (H + 15) // 16
         n_ss = tiles if B <= 4 else (tiles + 1) // 2         # one entry per GEMV workgroup (M > 4: tile pairs)
         merge_in_gemv = B <= self.FUSE_MAX_B
