@@ -144,6 +144,20 @@ int pg_decode_attn_block(const void* xq, const void* wqkv, void* qbuf, const PgF
  * (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
 int pg_decode_block_stamps(void* buf);
 
+/* Decode MLP block in ONE launch (batch <= 2, single rank, fragment-packed weights): the gate/up GEMV (x' = xq
+ * [M][H] from a PG_EPI_F32_FIN producer, rstd from its per-tile sums ss_in; gelu(gate)*up -> h [M][I] bf16) and the
+ * down GEMV split `ksplit` ways over K (write-through partials slab [ksplit][M][H] fp32, then the last-arriving split
+ * of each 16-column tile adds them into resid in split order, writes ss_out [M][ss_ld_out] and, with norm_w,
+ * fin_x = bf16(resid*(1+norm_w))).  Replaces GemmaMLP.forward (gemma.py:210-218) + the residual add (:413-418)
+ * of a decode step, i.e. pg_gemm_fused(gate/up, pro 4) + pg_gemm_fused(down, PG_EPI_F32_FIN, ksplit), with
+ * identical outputs.  Requires I/16 == (H/16)*ksplit (one workgroup per gate/up tile pair and per down unit).
+ * fin_cnt: H/16 zeroed tickets (self-resetting); sync: 18 zeroed ints (self-resetting; sync[17] = 1 if a wait
+ * timed out).  Returns hipErrorNotSupported with nothing launched when the grid cannot be co-resident. */
+int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld, int ss_n, float eps, const void* wgu,
+                        void* h, const void* wd, float* slab, int ksplit, int* fin_cnt, float* resid,
+                        float* ss_out, int ss_ld_out, void* fin_x, const float* norm_w, int* sync, int M, int H,
+                        int I, hipStream_t stream);
+
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
  * split-KV partials, merge with pg_attn_combine; kcap > 0 = readable cache rows (Smax, multiple of 32): each split's

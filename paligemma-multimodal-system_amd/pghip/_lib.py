@@ -39,6 +39,9 @@ SIGNATURES = {
     "pg_decode_attn_block": [vp, vp, vp, C.POINTER(PgFusedArgs), vp, vp, C.POINTER(PgFusedArgs), i32, i32, i32, vp, vp,
                              vp, vp],
     "pg_decode_block_stamps": [vp],
+    "pg_decode_mlp_stamps": [vp],
+    "pg_decode_mlp_block": [vp, vp, i32, i32, f32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
+                            vp],
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,

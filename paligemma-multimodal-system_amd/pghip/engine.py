@@ -89,6 +89,9 @@ class PaliGemmaEngine:
     # boundaries they remove, so it is off
     FUSE_BLOCK = os.environ.get("PG_FUSE_BLOCK", "0") == "1"
     BLOCK_SPLIT_O = int(os.environ.get("PG_BLOCK_SPLIT_O", "1"))   # o_proj split-K inside the block launch
+    # with USE_FIN, B <= FUSE_MAX_B: gate/up + down of a layer as ONE launch (pg_decode_mlp_block; the down
+    # projection split (I/16)/(H/16) = 8 ways, its weights issued while the h hand-off is in flight)
+    MLP_BLOCK = os.environ.get("PG_MLP_BLOCK", "0") == "1"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -101,9 +104,9 @@ class PaliGemmaEngine:
         self.split_o = self.DECODE_SPLIT_O if self.tp == 1 else 1        # smaller all-reduce messages under TP
         if os.environ.get("PG_SPLIT_O"):                                   # tuning overrides
             self.split_o = int(os.environ["PG_SPLIT_O"])
+        self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         if os.environ.get("PG_SPLIT_DOWN"):
             self.split_down = int(os.environ["PG_SPLIT_DOWN"])
-        self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         self.device = torch.device(device)
         self.image_token_id = cfg.get("image_token_index", 256000)
         pad = cfg.get("pad_token_id")
@@ -114,6 +117,7 @@ class PaliGemmaEngine:
         self._ws = {}
         self.graphs = {}
         self._block_ok = True      # pg_decode_attn_block accepted by this device (else the three-launch form)
+        self._mlp_ok = True        # pg_decode_mlp_block accepted by this device (else the two-launch form)
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name, shape, dtype):
@@ -478,6 +482,9 @@ class PaliGemmaEngine:
         sync = self._ws.get("d_block_sync")
         if sync is not None and int(sync[3].item()):
             raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
+        sync = self._ws.get("d_mlp_sync")
+        if sync is not None and int(sync[17].item()):
+            raise RuntimeError("pg_decode_mlp_block: an in-launch wait timed out")
 
     def _split_o(self, B: int) -> int:
         if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
@@ -546,10 +553,7 @@ class PaliGemmaEngine:
                     block = False
                 else:
                     nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-                    fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
-                    ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
-                    fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
-                    ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
+                    self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
                     continue
             if i == 0:      # the embedding rows are final: plain RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
@@ -584,11 +588,28 @@ class PaliGemmaEngine:
             else:
                 ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
-            ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
-            fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
-            ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
+            self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
         return xq, ss_d, tiles, n_ss
+
+    def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd):
+        """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
+        (x' of the next norm -> xq, its sums of squares -> ss_d).  One pg_decode_mlp_block launch at B <= FUSE_MAX_B
+        when the device holds its grid, else the two GEMV launches."""
+        w = self.w
+        if self.MLP_BLOCK and self._mlp_ok and B <= self.FUSE_MAX_B and w.frag:
+            H, I = w.hidden, w.inter
+            ks = (I // 16) // (H // 16) if (I // 16) % (H // 16) == 0 else 0
+            if 1 <= ks <= 8:
+                slab = self._buf("d_mlp_slab", (ks, B, H), torch.float32)
+                sync = self._zeros("d_mlp_sync", (18,), torch.int32)
+                if ops.decode_mlp_block(xq, ss_o, Lw["gu_w"], h, Lw["down_w"], slab, cnt, res, ss_d, sync, M=B,
+                                        ksplit=ks, fin_x=xq, norm_w=nxt_w):
+                    return
+            self._mlp_ok = False         # this shape / device: the two launches from now on
+        fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
+        ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+        fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+        ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
 
     def _split_keys(self, B: int, Smax: int) -> int:
         """Keys per decode-attention split: 32 (one MFMA block) at small batch; at B > FUSE_MAX_B (separate

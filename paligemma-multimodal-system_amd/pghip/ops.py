@@ -182,6 +182,28 @@ def decode_attn_block(xq, Wqkv, qbuf, fq, Wo, oslab, fo, *, ksplit_o: int, M: in
     return True
 
 
+def decode_mlp_block(xq, ss_in, Wgu, h, Wd, slab, fin_cnt, resid, ss_out, sync, *, M: int, ksplit: int,
+                     eps: float = 1e-6, fin_x=None, norm_w=None) -> bool:
+    """pg_decode_mlp_block: a decode layer's gate/up GEMV + down GEMV (split-K ksplit, finalised into resid) in one
+    launch.  ss_in / ss_out: [M][ld] per-tile sums of squares (ld = their row stride).  Returns False (nothing
+    launched) when the device cannot hold the whole grid at once; raises on any other error."""
+    _chk(Wgu, torch.bfloat16, "Wgu")
+    _chk(Wd, torch.bfloat16, "Wd")
+    _chk(sync, torch.int32, "sync")
+    _chk(fin_cnt, torch.int32, "fin_cnt")
+    H, I = Wd.shape
+    if Wgu.shape != (2 * I, H) or sync.numel() < 18 or slab.numel() < ksplit * M * H or h.numel() < M * I:
+        raise ValueError("pghip.decode_mlp_block: shapes do not match")
+    rc = _lib.load().pg_decode_mlp_block(_p(xq), _p(ss_in), ss_in.stride(0), H // 16, float(eps), _p(Wgu), _p(h),
+                                         _p(Wd), _p(slab), ksplit, _p(fin_cnt), _p(resid), _p(ss_out),
+                                         ss_out.stride(0), _p(fin_x), _p(norm_w), _p(sync), M, H, I, _s())
+    if rc == HIP_ERROR_NOT_SUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.PgHipError(f"pg_decode_mlp_block failed: hip error {rc} ({_lib._err_string(rc)})")
+    return True
+
+
 def attn_oproj(q, q_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, W, out, fa, sync, *, B, lkv_dev, Hq, Hkv, D,
                scale, split_keys, epi, ksplit, N=None, ldc=None):
     """pg_attn_oproj: split-KV decode attention computed inside the o_proj GEMV launch (fa.pro_mode = 5)."""

@@ -335,3 +335,37 @@ def test_pt224_fused_decode_block_bit_exact(golden):
     out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
     assert out[0].tolist() == runs[0][0]
     assert int(g["greedy_ids"][0]) == runs[0][0][0]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("B", [1, 2])
+def test_pt224_mlp_block_bit_exact(golden, B):
+    """pg_decode_mlp_block (a layer's gate/up GEMV + down GEMV as ONE launch, h handed over write-through inside the
+    launch, the down projection split 8 ways) against the two launches with the same down split (8): bit-identical
+    logits, tokens and KV cache over 12 full-size decode steps, no timed-out wait, every in-launch counter back at
+    zero; then the graph-replayed step reproduces the same tokens."""
+    from pghip import configs, engine, synthetic, weights
+    g = golden("pt224")
+    cfg = configs.PT_224
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+    ids = torch.from_numpy(g["input_ids"]).cuda().repeat(B, 1)
+    px = torch.from_numpy(g["pixel_values"]).cuda().repeat(B, 1, 1, 1)
+    runs = []
+    for block in (True, False):
+        eng.MLP_BLOCK, eng.split_down = block, 8
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
+        st = eng.decode_state(B, cache, nxt, 16)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
+        runs.append((st["hist"][:13].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
+    assert eng._mlp_ok
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
+    sync = eng._ws["d_mlp_sync"]
+    assert int(sync[17]) == 0 and int(sync[:17].abs().sum()) == 0
+    assert int(eng._ws["d_fin_cnt"].abs().sum()) == 0
+    eng.MLP_BLOCK, eng.split_down = type(eng).MLP_BLOCK, type(eng).DECODE_SPLIT_DOWN
+    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
+    assert out.tolist() == [[row[b] for row in runs[0][0]] for b in range(B)]
+    assert int(g["greedy_ids"][0]) == runs[0][0][0][0]
