@@ -151,7 +151,7 @@ int pg_decode_block_stamps(void* buf);
  * fin_x = bf16(resid*(1+norm_w))).  Replaces GemmaMLP.forward (gemma.py:210-218) + the residual add (:413-418)
  * of a decode step, i.e. pg_gemm_fused(gate/up, pro 4) + pg_gemm_fused(down, PG_EPI_F32_FIN, ksplit), with
  * identical outputs.  Requires I/16 == (H/16)*ksplit (one workgroup per gate/up tile pair and per down unit).
- * fin_cnt: H/16 zeroed tickets (self-resetting); sync: 18 zeroed ints (self-resetting; sync[17] = 1 if a wait
+ * fin_cnt: H/16 zeroed tickets (self-resetting); sync: 640 zeroed ints (self-resetting; sync[576] = 1 if a wait
  * timed out).  Returns hipErrorNotSupported with nothing launched when the grid cannot be co-resident. */
 int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld, int ss_n, float eps, const void* wgu,
                         void* h, const void* wd, float* slab, int ksplit, int* fin_cnt, float* resid,

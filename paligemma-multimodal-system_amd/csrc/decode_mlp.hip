@@ -31,9 +31,17 @@
 #ifndef PG_MLP_D_DEPTH
 #define PG_MLP_D_DEPTH 8                   // down chunks in flight per wave (8 = the whole unit)
 #endif
+#ifndef PG_MLP_SLEEP
+#define PG_MLP_SLEEP 32                    // s_sleep between polls (x 64 cycles)
+#endif
+#ifndef PG_MLP_CSTRIDE
+#define PG_MLP_CSTRIDE 64                  // ints between the slice counters: one 256-B line each (polls that share
+                                           // a line with the arrivals measured 2x slower: 98 vs 45 us per layer)
+#endif
 #define MLP_XPAD 8
-#define MLP_SYNC_DONE 16
-#define MLP_SYNC_ERR 17
+#define MLP_SYNC_DONE (8 * PG_MLP_CSTRIDE)          // after the (<= 8) slice counters, each on a line of its own
+#define MLP_SYNC_ERR (8 * PG_MLP_CSTRIDE + 64)
+#define MLP_SYNC_INTS (8 * PG_MLP_CSTRIDE + 128)    // pg_decode_mlp_block's sync buffer size (ints)
 
 struct MlpBlockArgs {
   const bf16_t* xq;      // [M][H] x' = bf16(resid * (1 + post_w)) (the o_proj F32_FIN epilogue, previous launch)
@@ -50,7 +58,7 @@ struct MlpBlockArgs {
   int ss_ld_out;
   bf16_t* fin_x;         // [M][H] x' = bf16(resid * (1 + norm_w)) for the next GEMV (may be null)
   const float* norm_w;   // the next RMSNorm's weight (with fin_x)
-  int* sync;             // [0, KS) slice arrivals, [16] workgroups done, [17] err; zero before the first launch
+  int* sync;             // slice arrivals [z * CSTRIDE], workgroups done, err (MLP_SYNC_*); zero before the first launch
   int M, H, I, KS;
   unsigned long long* stamps;   // diagnostics (pg_decode_mlp_stamps): [workgroup][4] wall-clock stamps, or null
 };
@@ -166,7 +174,7 @@ __device__ __forceinline__ void mlp_gate_up(const MlpBlockArgs& a, int p, f32x4 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const int per_slice = (a.I / 16) / a.KS;
-  if (lane == 0) __hip_atomic_fetch_add(a.sync + p / per_slice, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) __hip_atomic_fetch_add(a.sync + (p / per_slice) * PG_MLP_CSTRIDE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (a.stamps && lane == 0) a.stamps[(size_t)p * 4 + 1] = wall_clock64();
 }
 
@@ -195,12 +203,12 @@ __device__ __forceinline__ void mlp_down(const MlpBlockArgs& a, int t, int z, bf
   const int per_slice = (a.I / 16) / a.KS;
   if (threadIdx.x == 0) {
     const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(a.sync + z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < per_slice) {
+    while (__hip_atomic_load(a.sync + z * PG_MLP_CSTRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < per_slice) {
       if (wall_clock64() - t0 > PG_MLP_TIMEOUT_TICKS) {
         __hip_atomic_store(a.sync + MLP_SYNC_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(PG_MLP_SLEEP);
     }
     if (a.stamps) a.stamps[(size_t)blockIdx.x * 4 + 2] = wall_clock64();
   }
@@ -290,7 +298,8 @@ __global__ __launch_bounds__(256) void decode_mlp_kernel(MlpBlockArgs a) {
     // every wait of this workgroup is over: the last one to get here resets the counters for the next launch
     if (__hip_atomic_fetch_add(a.sync + MLP_SYNC_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
         (int)gridDim.x - 1) {
-      for (int i = 0; i < a.KS; ++i) __hip_atomic_store(a.sync + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < a.KS; ++i)
+        __hip_atomic_store(a.sync + i * PG_MLP_CSTRIDE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.sync + MLP_SYNC_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (a.stamps) a.stamps[(size_t)p * 4 + 3] = wall_clock64();
@@ -322,6 +331,7 @@ extern "C" int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld
                                    float* ss_out, int ss_ld_out, void* fin_x, const float* norm_w, int* sync, int M,
                                    int H, int I, hipStream_t stream) {
   PG_REQUIRE(xq && ss_in && wgu && h && wd && slab && fin_cnt && resid && ss_out && sync);
+  static_assert(MLP_SYNC_INTS <= 640, "pg_decode_mlp_block documents a 640-int sync buffer");
   PG_REQUIRE(M >= 1 && M <= 2 && ss_n > 0 && ss_ld >= ss_n && ss_n <= 256 && (M == 1 || ss_n <= 128));
   PG_REQUIRE(H % 16 == 0 && I % 16 == 0 && ksplit >= 1 && ksplit <= 8 && (I / 16) == (H / 16) * ksplit);
   PG_REQUIRE(ss_ld_out >= H / 16 && (fin_x == nullptr || norm_w != nullptr));

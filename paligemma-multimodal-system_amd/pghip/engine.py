@@ -483,7 +483,7 @@ class PaliGemmaEngine:
         if sync is not None and int(sync[3].item()):
             raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
         sync = self._ws.get("d_mlp_sync")
-        if sync is not None and int(sync[17].item()):
+        if sync is not None and int(sync[576].item()):
             raise RuntimeError("pg_decode_mlp_block: an in-launch wait timed out")
 
     def _split_o(self, B: int) -> int:
@@ -601,7 +601,7 @@ class PaliGemmaEngine:
             ks = (I // 16) // (H // 16) if (I // 16) % (H // 16) == 0 else 0
             if 1 <= ks <= 8:
                 slab = self._buf("d_mlp_slab", (ks, B, H), torch.float32)
-                sync = self._zeros("d_mlp_sync", (18,), torch.int32)
+                sync = self._zeros("d_mlp_sync", (640,), torch.int32)
                 if ops.decode_mlp_block(xq, ss_o, Lw["gu_w"], h, Lw["down_w"], slab, cnt, res, ss_d, sync, M=B,
                                         ksplit=ks, fin_x=xq, norm_w=nxt_w):
                     return

@@ -192,7 +192,7 @@ def decode_mlp_block(xq, ss_in, Wgu, h, Wd, slab, fin_cnt, resid, ss_out, sync, 
     _chk(sync, torch.int32, "sync")
     _chk(fin_cnt, torch.int32, "fin_cnt")
     H, I = Wd.shape
-    if Wgu.shape != (2 * I, H) or sync.numel() < 18 or slab.numel() < ksplit * M * H or h.numel() < M * I:
+    if Wgu.shape != (2 * I, H) or sync.numel() < 640 or slab.numel() < ksplit * M * H or h.numel() < M * I:
         raise ValueError("pghip.decode_mlp_block: shapes do not match")
     rc = _lib.load().pg_decode_mlp_block(_p(xq), _p(ss_in), ss_in.stride(0), H // 16, float(eps), _p(Wgu), _p(h),
                                          _p(Wd), _p(slab), ksplit, _p(fin_cnt), _p(resid), _p(ss_out),

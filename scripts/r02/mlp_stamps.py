@@ -12,6 +12,7 @@ import bench  # noqa: E402
 
 cfg = configs.CONFIGS["pt-224"]
 eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+eng.MLP_BLOCK = True
 ids, px = bench.synthetic_inputs(cfg, 1, [2, 651, 4906, 603, 476, 2121, 576, 108])
 ids, px = ids.cuda(), px.cuda()
 cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 40)

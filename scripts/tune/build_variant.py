@@ -1,0 +1,25 @@
+"""Link a tuning variant of libpghip.so: recompile ONE source with extra -D defines, reuse the product build's
+other objects (paligemma-multimodal-system_amd/build/obj).
+
+    python scripts/tune/build_variant.py out.so decode_mlp.hip PG_MLP_D_DEPTH=2 [...]
+"""
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "paligemma-multimodal-system_amd"))
+from pghip import build  # noqa: E402
+
+out, src, defs = sys.argv[1], sys.argv[2], sys.argv[3:]
+build.build()
+vdir = os.path.join(build.OBJ_DIR, "v_" + os.path.basename(out).replace(".so", ""))
+os.makedirs(vdir, exist_ok=True)
+obj = build._compile(os.path.join(build.CSRC, src), vdir, defs)
+objs = [o for o in sorted(glob.glob(os.path.join(build.OBJ_DIR, "*.o"))) if os.path.basename(o) != src + ".o"]
+r = subprocess.run([build.HIPCC, f"--offload-arch={build.ARCH}", "-shared", "-fPIC", *objs, obj, "-o", out],
+                   capture_output=True, text=True)
+if r.returncode:
+    raise SystemExit(r.stderr)
+print("built", out, defs)

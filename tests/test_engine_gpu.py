@@ -363,7 +363,7 @@ def test_pt224_mlp_block_bit_exact(golden, B):
     assert torch.equal(runs[0][1], runs[1][1])
     assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
     sync = eng._ws["d_mlp_sync"]
-    assert int(sync[17]) == 0 and int(sync[:17].abs().sum()) == 0
+    assert int(sync[576]) == 0 and int(sync.abs().sum()) == 0
     assert int(eng._ws["d_fin_cnt"].abs().sum()) == 0
     eng.MLP_BLOCK, eng.split_down = type(eng).MLP_BLOCK, type(eng).DECODE_SPLIT_DOWN
     out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
