@@ -28,6 +28,9 @@
 #ifndef PG_COMBINE_PF
 #define PG_COMBINE_PF 12  // split-KV merge: O partials of the first 12 splits per thread loaded up front
 #endif
+#ifndef PG_ATTN_WG
+#define PG_ATTN_WG 1      // decode splits of 2 / 4 / 8 blocks (head_dim 256): one wave per block, merged in LDS
+#endif
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
@@ -38,6 +41,57 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(AttnArgs a) {
   const int nsplit = (int)gridDim.y / a.Hkv;
   attn_decode_split<DP, DT, false, FULL>(a, blockIdx.z, blockIdx.y / nsplit, blockIdx.y % nsplit, nsplit,
                                          threadIdx.x);
+}
+
+// Decode (split mode) with NW-block splits (split_keys = 32 * NW): one workgroup of NW waves per (batch, kv head,
+// split), wave w takes the split's 32-key block w (all blocks' loads in flight at once, one memory round trip
+// instead of NW sequential ones), and the waves' (O, m, l) are merged through LDS into ONE partial of the split
+// (2^(m_w - M) weights, the merge of pg_attn_combine), so the combine still sees nsplit partials.  Needs a known
+// cache capacity (kcap >= 32) and head_dim == DP.  grid (1, Hkv * nsplit, B).
+template <int DP, int DT, int NW>
+__global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
+  const int nsplit = (int)gridDim.y / a.Hkv;
+  const int b = blockIdx.z, kvh = blockIdx.y / nsplit, sp = blockIdx.y % nsplit;
+  f32x4 o[DT];
+  float m, l;
+  attn_decode_block32<DP, DT>(a, b, kvh, sp * a.split_keys + 32 * wave, lane, o, m, l);
+  __shared__ f32x4 so[NW - 1][DT][64];
+  __shared__ float sml[NW - 1][2][16];
+  if (wave > 0) {
+#pragma unroll
+    for (int t = 0; t < DT; ++t) so[wave - 1][t][lane] = o[t];
+    if (g == 0) {
+      sml[wave - 1][0][c] = m;
+      sml[wave - 1][1][c] = l;
+    }
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  float M = m;
+#pragma unroll
+  for (int w = 0; w < NW - 1; ++w) M = fmaxf(M, sml[w][0][c]);
+  const float w0 = m == -INFINITY ? 0.f : exp2f(m - M);
+  float L = l * w0;
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] *= w0;
+#pragma unroll
+  for (int w = 0; w < NW - 1; ++w) {
+    const float mw = sml[w][0][c];
+    const float ww = mw == -INFINITY ? 0.f : exp2f(mw - M);
+    L += ww * sml[w][1][c];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] += ww * so[w][t][lane];
+  }
+  if (c >= a.Lq * a.G) return;                   // rows past Lq*G are never merged
+  const long base = (((long)b * a.Hkv + kvh) * nsplit + sp) * 16 + c;
+  float* po = a.part_o + base * (DT * 16);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) *(f32x4*)(po + 16 * t + 4 * g) = o[t];
+  if (g == 0) {
+    a.part_ml[base * 2 + 0] = M;
+    a.part_ml[base * 2 + 1] = L;
+  }
 }
 
 template <int DP, int DT>
@@ -654,7 +708,15 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
       launch_fa<DP_, DT_>(fa_waves, fa_rpw, grid, stream, a);                                \
     else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
-    else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32)           \
+    else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32 && PG_ATTN_WG && DP_ == 256 && \
+             (split_keys == 64 || split_keys == 128 || split_keys == 256)) {                 \
+      if (split_keys == 64)                                                                  \
+        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 2>), grid, dim3(128), 0, stream, a); \
+      else if (split_keys == 128)                                                            \
+        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 4>), grid, dim3(256), 0, stream, a); \
+      else                                                                                   \
+        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 8>), grid, dim3(512), 0, stream, a); \
+    } else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32)         \
       hipLaunchKernelGGL((attn_decode_kernel<DP_, DT_, true>), grid, dim3(64), 0, stream, a); \
     else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1)                                     \
       hipLaunchKernelGGL((attn_decode_kernel<DP_, DT_, false>), grid, dim3(64), 0, stream, a); \

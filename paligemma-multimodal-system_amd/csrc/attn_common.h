@@ -296,3 +296,92 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     }
   }
 }
+
+// One 32-key block [kb, kb + 32) of a decode split, one wave, head_dim == DP, known cache capacity (a.kcap >= 32):
+// the block's K rows and V^T runs are issued before the kv length is read (rows past it masked after they land),
+// exactly as attn_decode_split's FULL first block, and its (O^T, m, l) are returned in registers (lane holds
+// O^T[d = 16t + 4g + j][q = c]; m, l of row c) for a caller that merges several blocks (attn_decode_wg_kernel).
+template <int DP, int DT>
+__device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, int kvh, int kb, int lane,
+                                                    f32x4 (&o)[DT], float& m, float& l) {
+  constexpr int KS = DP / 32;
+  const int c = lane & 15, g = lane >> 4;
+  const int R = a.Lq * a.G;
+  const int rr = c < R ? c : R - 1;              // rows past Lq*G read row R - 1 (never stored): no select
+  const int pos = rr / a.G;
+  const int hq = kvh * a.G + rr % a.G;
+  const int lkv_raw =
+      __hip_atomic_load(a.lkv_dev ? a.lkv_dev : &pg_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bf16x8 qf[KS];
+  const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * DP;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qf[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qp + 32 * s + 8 * g));
+  const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
+  const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
+  // a block past the cache reads the last block (never used: all its keys are masked)
+  const int kl = min(kb, a.kcap - 32);
+  u32x4 kfa[KS], kfb[KS];
+  u32x2 vr[DT][2];
+  {
+    const bf16_t* pa = kbase + (long)(kl + c) * a.k_rs;
+    const bf16_t* pb = kbase + (long)(kl + 16 + c) * a.k_rs;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      kfa[s] = *(const u32x4*)(pa + 32 * s + 8 * g);
+      kfb[s] = *(const u32x4*)(pb + 32 * s + 8 * g);
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
+      vr[t][0] = *(const u32x2*)(vrow + kl + 4 * g);
+      vr[t][1] = *(const u32x2*)(vrow + kl + 16 + 4 * g);
+    }
+  }
+  // every load of the block is issued before its first use (one memory round trip)
+  __builtin_amdgcn_sched_barrier(0);
+  const int Lkv = __builtin_amdgcn_readfirstlane(lkv_raw) + a.Lkv;
+  const int kend = min(Lkv, kb + 32);
+  u32x4 vf[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    const int n0 = kend - (kb + 4 * g), n1 = kend - (kb + 16 + 4 * g);   // valid keys among each run of 4
+    const u32x2 v0 = vr[t][0], v1 = vr[t][1];
+    vf[t] = u32x4{n0 >= 2 ? v0[0] : (n0 == 1 ? (v0[0] & 0xFFFFu) : 0u),
+                  n0 >= 4 ? v0[1] : (n0 == 3 ? (v0[1] & 0xFFFFu) : 0u),
+                  n1 >= 2 ? v1[0] : (n1 == 1 ? (v1[0] & 0xFFFFu) : 0u),
+                  n1 >= 4 ? v1[1] : (n1 == 3 ? (v1[1] & 0xFFFFu) : 0u)};
+  }
+  f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    sA = mfma16(__builtin_bit_cast(bf16x8, kfa[s]), qf[s], sA);
+    sB = mfma16(__builtin_bit_cast(bf16x8, kfb[s]), qf[s], sB);
+  }
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[j] = kb + 4 * g + j < kend ? sA[j] * a.scale_log2 : -INFINITY;
+    x[4 + j] = kb + 16 + 4 * g + j < kend ? sB[j] * a.scale_log2 : -INFINITY;
+  }
+  float bm = x[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
+  bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  const bool none = bm == -INFINITY;            // every key of the block masked
+  float rs = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - bm); rs += x[j]; }
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  m = bm;
+  l = rs;
+  u32x4 pw;
+  pw[0] = pack_bf2(x[0], x[1]);
+  pw[1] = pack_bf2(x[2], x[3]);
+  pw[2] = pack_bf2(x[4], x[5]);
+  pw[3] = pack_bf2(x[6], x[7]);
+  const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, f32x4{0.f, 0.f, 0.f, 0.f});
+}

@@ -26,6 +26,9 @@
 #ifndef PG_G256_STAGGER
 #define PG_G256_STAGGER 1       // gemm256: wave groups one barrier apart (MFMA of one || LDS reads of the other); +4-14%
 #endif
+#ifndef PG_SKINNY
+#define PG_SKINNY 0             // prefill GEMMs of 161..288 rows as one 256- or 288-row tile per 128 columns
+#endif
 #ifndef PG_G256_PREFETCH
 #define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
 #endif
@@ -329,6 +332,7 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
     case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
     case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
     case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
@@ -344,7 +348,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
   constexpr int W_BYTES = TBN * TBK * 2;
   constexpr int STAGE_BYTES = A_BYTES + W_BYTES;
   constexpr int P = BM / 32 + TBN / 32;            // glds pieces per wave per stage
-  constexpr int WN = BM == 64 ? 4 : 2;             // waves along N
+  constexpr int WN = BM == 64 ? 4 : 2;             // waves along N (BM 256 / 288: 2 x 2 waves of 128 / 144 rows)
   constexpr int WM = 4 / WN;                       // waves along M
   constexpr int NI = BM / WM / 16;                 // 16-row subtiles per wave
   constexpr int NJ = TBN / WN / 16;                // 16-col subtiles per wave
@@ -1441,6 +1445,21 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
+  if constexpr (!F8) {
+    if (PG_SKINNY && e.M > 160 && e.M <= 288) {
+      // skinny prefill (batch 1: 256 image + a few text rows): ALL rows in one tile, so every weight tile streams
+      // once and no 256-row tile is spent on an 8-row remainder (M = 264: 2 x 256 rows in gemm256)
+      const int tiles_n = (e.N + TBN - 1) / TBN;
+      const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
+      if (e.M <= 256)
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 256, 3, FRAG>), dim3(tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+                           W, ldw, K, kchunk, 1, tiles_n, e);
+      else
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 288, 3, FRAG>), dim3(tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+                           W, ldw, K, kchunk, 1, tiles_n, e);
+      return;
+    }
+  }
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
   if ((PG_F8_G256 || !F8) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;

@@ -57,8 +57,18 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    # incremental: a source is recompiled when it, or any header, is newer than its object (gemm.hip alone takes
+    # minutes); a tuning variant (defines) always compiles everything
+    hdr = max([os.path.getmtime(p) for p in glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))]
+              or [0.0])
+
+    def obj_for(src):
+        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if (defines or force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr)):
+            return _compile(src, obj_dir, defines)
+        return obj
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, obj_dir, defines), srcs))
+        objs = list(ex.map(obj_for, srcs))
     tmp = out + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     r = subprocess.run(cmd, capture_output=True, text=True)

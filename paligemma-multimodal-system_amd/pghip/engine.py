@@ -619,7 +619,9 @@ class PaliGemmaEngine:
         if B <= self.FUSE_MAX_B:
             return SK
         blocks = (Smax + SK - 1) // SK
-        return SK * max(1, min(8, (B * blocks) // self.DECODE_SPLIT_TARGET))
+        mult = max(1, min(8, (B * blocks) // self.DECODE_SPLIT_TARGET))
+        # a power of two: 2 / 4 / 8-block splits run one wave per block, merged in LDS (attn_decode_wg_kernel)
+        return SK * (1 << (mult.bit_length() - 1))
 
     def _decode_layers_unfused(self, st, cache, res, xn, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t,
                                SK=None):

@@ -266,14 +266,23 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     ops.attn_combine(po, pml, od, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
     assert err(od, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2
     # kcap = Smax: every split's first block is loaded before the kv length is read (rows past it masked after
-    # the loads land): bit-identical partials and output
-    if Smax % 32 == 0:
-        po2, pml2, od2 = torch.empty_like(po), torch.empty_like(pml), torch.empty_like(od)
-        ops.attention(qd, nh * hd, od2, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
-                      B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=SK,
-                      nsplit=nsplit, part_o=po2, part_ml=pml2, kcap=Smax)
-        ops.attn_combine(po2, pml2, od2, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
-        assert torch.equal(od2, od)
+    # the loads land).  One-block splits (32 keys): bit-identical to the kcap = 0 kernel.  2 / 4 / 8-block splits
+    # at head_dim 256 run one wave per block merged in LDS (attn_decode_wg_kernel): same bound as above.
+    for sk in (32, 64, 128, 256):
+        ns = ((Smax + sk - 1) // sk + 3) // 4 * 4
+        po1 = torch.empty(B * nkv * ns * 16 * dt, device="cuda")
+        pml1 = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
+        outs = []
+        for kcap in (0, Smax):
+            od2 = torch.empty_like(od)
+            ops.attention(qd, nh * hd, od2, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
+                          B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=sk,
+                          nsplit=ns, part_o=po1, part_ml=pml1, kcap=kcap)
+            ops.attn_combine(po1, pml1, od2, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=ns)
+            assert err(od2, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2, (sk, kcap)
+            outs.append(od2)
+        if sk == 32:
+            assert torch.equal(outs[0], outs[1])
 
 
 def test_rope_kv_write_matches_reference_formula():
