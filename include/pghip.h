@@ -158,6 +158,10 @@ int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld, int ss_n,
                         float* ss_out, int ss_ld_out, void* fin_x, const float* norm_w, int* sync, int M, int H,
                         int I, hipStream_t stream);
 
+/* Diagnostics: every later pg_decode_mlp_block launch records per workgroup [start, h published, h slice ready,
+ * end] (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
+int pg_decode_mlp_stamps(void* buf);
+
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
  * split-KV partials, merge with pg_attn_combine; kcap > 0 = readable cache rows (Smax, multiple of 32): each split's
