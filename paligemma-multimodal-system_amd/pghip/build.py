@@ -57,10 +57,10 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
-    # incremental: a source is recompiled when it, or any header, is newer than its object (gemm.hip alone takes
-    # minutes); a tuning variant (defines) always compiles everything
-    hdr = max([os.path.getmtime(p) for p in glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))]
-              or [0.0])
+    # incremental: a source is recompiled when it, or any csrc header, is newer than its object (gemm.hip alone
+    # takes minutes; include/pghip.h is the C-ABI declaration, included by no source); a tuning variant (defines)
+    # always compiles everything
+    hdr = max([os.path.getmtime(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] or [0.0])
 
     def obj_for(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
