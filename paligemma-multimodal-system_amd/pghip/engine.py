@@ -66,7 +66,7 @@ class PaliGemmaEngine:
     DECODE_SPLIT_O = 2      # split-K of o_proj at decode (B > FUSE_MAX_B: more workgroups for the batched GEMV)
     DECODE_SPLIT_O_SMALL = 1  # ... at B <= FUSE_MAX_B: unsplit, the GEMV finalises its own tile (no slab, no ticket;
                               # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
-    DECODE_SPLIT_DOWN = 4   # split-K of down_proj at decode
+    DECODE_SPLIT_DOWN = 8   # split-K of down_proj at decode (8 vs 4: -4..6 us per pt-224 step, scripts/r02/gpu_t.sh)
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
