@@ -158,6 +158,21 @@ int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld, int ss_n,
                         float* ss_out, int ss_ld_out, void* fin_x, const float* norm_w, int* sync, int M, int H,
                         int I, hipStream_t stream);
 
+/* Decode MLP engine (batch 1, Gemma-2B shapes, single rank): the same computation as pg_decode_mlp_block as one
+ * persistent launch of 256 two-wave workgroups (one per CU): a loader wave streams the CU's gate/up and down weight
+ * slices into a ring of LDS slots by LDS-DMA (running ahead of every dependency), a consumer wave multiplies out of
+ * LDS; h is handed over as 8-byte {bf16 pair, epoch tag} granules (hgran: I/2 u64, any initial content), the down
+ * projection is split in two k-halves (slab: 2*H fp32) and the second-arriving half finalises the tile into resid,
+ * ss_out (H/16) and fin_x.  fin_cnt: H/16 zeroed ints; sync: 192 zeroed ints (self-managing; sync[128] = 1 if a
+ * wait timed out).  Replaces gemma.py:210-218 + :413-418 of a decode step.  Returns hipErrorNotSupported with
+ * nothing launched for other shapes or when one workgroup per CU cannot cover the 256-workgroup grid. */
+int pg_decode_mlp_engine(const void* xq, const float* ss_in, int ss_n, float eps, const void* wgu, const void* wd,
+                         void* hgran, float* slab, int* fin_cnt, float* resid, float* ss_out, void* fin_x,
+                         const float* norm_w, int* sync, int M, int H, int I, hipStream_t stream);
+/* Diagnostics: every later pg_decode_mlp_engine launch records per CU [start, h published, h half gathered,
+ * down done, end, -, -, -] (100 MHz wall clock, u64) into buf [256][8]; null turns it off. */
+int pg_decode_mlp_engine_stamps(void* buf);
+
 /* Diagnostics: every later pg_decode_mlp_block launch records per workgroup [start, h published, h slice ready,
  * end] (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
 int pg_decode_mlp_stamps(void* buf);

@@ -40,6 +40,8 @@ SIGNATURES = {
                              vp, vp],
     "pg_decode_block_stamps": [vp],
     "pg_decode_mlp_stamps": [vp],
+    "pg_decode_mlp_engine": [vp, vp, i32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
+    "pg_decode_mlp_engine_stamps": [vp],
     "pg_decode_mlp_block": [vp, vp, i32, i32, f32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
                             vp],
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],

@@ -92,6 +92,8 @@ class PaliGemmaEngine:
     # with USE_FIN, B <= FUSE_MAX_B: gate/up + down of a layer as ONE launch (pg_decode_mlp_block; the down
     # projection split (I/16)/(H/16) = 8 ways, its weights issued while the h hand-off is in flight)
     MLP_BLOCK = os.environ.get("PG_MLP_BLOCK", "0") == "1"
+    # B = 1: gate/up + down as one persistent loader / consumer launch (pg_decode_mlp_engine, csrc/decode_engine.hip)
+    MLP_ENGINE = os.environ.get("PG_MLP_ENGINE", "0") == "1"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -118,6 +120,7 @@ class PaliGemmaEngine:
         self.graphs = {}
         self._block_ok = True      # pg_decode_attn_block accepted by this device (else the three-launch form)
         self._mlp_ok = True        # pg_decode_mlp_block accepted by this device (else the two-launch form)
+        self._engine_ok = True     # pg_decode_mlp_engine accepted by this device
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name, shape, dtype):
@@ -482,6 +485,9 @@ class PaliGemmaEngine:
         sync = self._ws.get("d_block_sync")
         if sync is not None and int(sync[3].item()):
             raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
+        sync = self._ws.get("d_en_sync")
+        if sync is not None and int(sync[128].item()):
+            raise RuntimeError("pg_decode_mlp_engine: an in-launch wait timed out")
         sync = self._ws.get("d_mlp_sync")
         if sync is not None and int(sync[576].item()):
             raise RuntimeError("pg_decode_mlp_block: an in-launch wait timed out")
@@ -596,6 +602,16 @@ class PaliGemmaEngine:
         (x' of the next norm -> xq, its sums of squares -> ss_d).  One pg_decode_mlp_block launch at B <= FUSE_MAX_B
         when the device holds its grid, else the two GEMV launches."""
         w = self.w
+        if self.MLP_ENGINE and self._engine_ok and B == 1 and w.frag:
+            H, I = w.hidden, w.inter
+            hg = self._buf("d_en_h", (I // 2,), torch.int64)
+            slab = self._buf("d_en_slab", (2, H), torch.float32)
+            tk = self._zeros("d_en_cnt", (H // 16,), torch.int32)
+            sync = self._zeros("d_en_sync", (192,), torch.int32)
+            if ops.decode_mlp_engine(xq, ss_o, Lw["gu_w"], Lw["down_w"], hg, slab, tk, res, ss_d, sync, fin_x=xq,
+                                     norm_w=nxt_w):
+                return
+            self._engine_ok = False
         if self.MLP_BLOCK and self._mlp_ok and B <= self.FUSE_MAX_B and w.frag:
             H, I = w.hidden, w.inter
             ks = (I // 16) // (H // 16) if (I // 16) % (H // 16) == 0 else 0

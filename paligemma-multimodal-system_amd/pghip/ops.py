@@ -204,6 +204,27 @@ def decode_mlp_block(xq, ss_in, Wgu, h, Wd, slab, fin_cnt, resid, ss_out, sync, 
     return True
 
 
+def decode_mlp_engine(xq, ss_in, Wgu, Wd, hgran, slab, fin_cnt, resid, ss_out, sync, *, eps: float = 1e-6,
+                      fin_x=None, norm_w=None) -> bool:
+    """pg_decode_mlp_engine: a batch-1 decode layer's gate/up + down GEMVs as one persistent loader / consumer
+    launch (one workgroup per CU).  Returns False (nothing launched) for shapes or devices it does not cover."""
+    _chk(Wgu, torch.bfloat16, "Wgu")
+    _chk(Wd, torch.bfloat16, "Wd")
+    _chk(sync, torch.int32, "sync")
+    _chk(fin_cnt, torch.int32, "fin_cnt")
+    H, I = Wd.shape
+    if Wgu.shape != (2 * I, H) or sync.numel() < 192 or slab.numel() < 2 * H or hgran.numel() * hgran.element_size() < I * 4:
+        raise ValueError("pghip.decode_mlp_engine: shapes do not match")
+    rc = _lib.load().pg_decode_mlp_engine(_p(xq), _p(ss_in), H // 16, float(eps), _p(Wgu), _p(Wd), _p(hgran),
+                                          _p(slab), _p(fin_cnt), _p(resid), _p(ss_out), _p(fin_x), _p(norm_w),
+                                          _p(sync), 1, H, I, _s())
+    if rc == HIP_ERROR_NOT_SUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.PgHipError(f"pg_decode_mlp_engine failed: hip error {rc} ({_lib._err_string(rc)})")
+    return True
+
+
 def attn_oproj(q, q_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, W, out, fa, sync, *, B, lkv_dev, Hq, Hkv, D,
                scale, split_keys, epi, ksplit, N=None, ldc=None):
     """pg_attn_oproj: split-KV decode attention computed inside the o_proj GEMV launch (fa.pro_mode = 5)."""

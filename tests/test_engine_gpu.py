@@ -369,3 +369,37 @@ def test_pt224_mlp_block_bit_exact(golden, B):
     out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
     assert out.tolist() == [[row[b] for row in runs[0][0]] for b in range(B)]
     assert int(g["greedy_ids"][0]) == runs[0][0][0][0]
+
+
+@pytest.mark.slow
+def test_pt224_mlp_engine_matches_two_launches(golden):
+    """pg_decode_mlp_engine (a batch-1 layer's gate/up + down GEMVs as one persistent loader / consumer launch, h
+    handed over as tagged granules, the down projection in two k-halves) against the two GEMV launches: 12
+    full-size decode steps from the same prefill, per-step logits within 1e-2 of their scale (a different fp32
+    summation order and split), the same greedy ids, no timed-out wait, the tickets back at zero and the epoch
+    advanced once per launch; then the graph-replayed step reproduces the same ids."""
+    from pghip import configs, engine, synthetic, weights
+    g = golden("pt224")
+    cfg = configs.PT_224
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+    ids = torch.from_numpy(g["input_ids"]).cuda()
+    px = torch.from_numpy(g["pixel_values"]).cuda()
+    runs = []
+    for on in (True, False):
+        eng.MLP_ENGINE = on
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
+        st = eng.decode_state(1, cache, nxt, 16)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
+        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg)))
+    assert eng._engine_ok
+    assert runs[0][0] == runs[1][0]
+    for t in range(12):
+        assert err(runs[0][1][t].cpu().numpy(), runs[1][1][t].cpu().numpy()) < 1e-2, t
+    sync = eng._ws["d_en_sync"]
+    assert int(sync[128]) == 0 and int(sync[64]) == 0 and int(sync[0]) == 12 * 18
+    assert int(eng._ws["d_en_cnt"].abs().sum()) == 0
+    eng.MLP_ENGINE = True
+    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
+    eng.MLP_ENGINE = type(eng).MLP_ENGINE
+    assert out[0].tolist() == runs[0][0]
