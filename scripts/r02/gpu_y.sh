@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r02y; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_engine_gpu.py -k "mlp_engine" > $O/test.log 2>&1 || { tail -15 $O/test.log; exit 1; }
 tail -1 $O/test.log
-for v in base thin0 gs8; do
+for v in base; do
   if [ $v = base ]; then L=""; else L=scripts/tune/en_$v.so; fi
   PGHIP_LIB=$L timeout -k 10 200 python scripts/r02/engine_stamps.py > $O/stamps_$v.txt 2> $O/err.log || { tail -5 $O/err.log; exit 1; }
   PGHIP_LIB=$L PG_MLP_ENGINE=1 timeout -k 10 200 python scripts/tune/decode_step.py --steps 50 > $O/step_$v.json 2> $O/err.log || { tail -5 $O/err.log; exit 1; }
