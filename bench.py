@@ -150,8 +150,8 @@ class Runner:
         self.state = state = {}
         mask = torch.ones_like(ids)
         cache, feats, logits, nxt = eng.prefill_request(ids, px, mask, T)
-        st = eng.decode_state(B, cache, nxt, T)
-        eng.sample(logits, st, sampler, advance=False)
+        st = eng.decode_state(B, cache, nxt, T, sampler=sampler)
+        eng.sample(logits, st, sampler, advance=False, feats=feats)
         state.update(cache=cache, feats=feats, st=st)
         try:
             if not eng.comm.capturable:
@@ -177,7 +177,7 @@ class Runner:
             state["st"]["kv_len"].fill_(L)
             state["st"]["step"].zero_()
             state["feats"].copy_(f)
-            eng.sample(lg, state["st"], sampler, advance=False)
+            eng.sample(lg, state["st"], sampler, advance=False, feats=state["feats"])
 
         # optionally the prefill's ~400 launches as one hipGraph (fixed request shape, as a serving replica would
         # hold one per shape bucket); measured slower than eager launches on MI355X (pt-224 6.0 vs 5.76 ms,

@@ -210,6 +210,13 @@ int pg_embed_merge(const int64_t* ids, const int* rank, int n, const void* embed
  * hist[*step][b] = token (only while *step < hist_rows), pos[b] += 1, *kv_len += 1, *step += 1. */
 int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
               int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, hipStream_t stream);
+/* pg_argmax, then the next decode step's input rows res[b] = pg_embed_merge of the winners (rank = nullptr:
+ * image-token rank = count of earlier rows whose winner is the image token), in the same final launch;
+ * the chained greedy loop of inference.py:59-80 then needs no separate embed launch per step.  B <= 1024. */
+int pg_argmax_embed(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
+                    int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, const void* embed, int V_embed,
+                    const float* feat, int n_feat, int H, long image_id, long pad_id, float img_scale,
+                    float normalizer, float* res, hipStream_t stream);
 
 /* vocabulary-parallel greedy for tensor parallelism: local (max, first global index) pairs [B][2] of a
  * vocab shard starting at vocab_offset; after an all-gather, pg_argmax_merge takes the global winner

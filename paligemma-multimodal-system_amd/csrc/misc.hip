@@ -6,6 +6,7 @@
 //   pg_rope_kv_write  : RoPE on q (in place) and k, append k / v^T to the static KV cache
 //                       (modeling_gemma.py:112-151, KVCache.update :18-57)
 //   pg_argmax         : greedy next token, first index on ties (inference.py:68)
+//   pg_argmax_embed   : pg_argmax + the next step's input rows (the embed of the next decode step folded in)
 //   pg_topp_sample    : temperature softmax + top-p filter + explicit-uniform draw (inference.py:65,90-106)
 //   pg_synth_fill     : name-seeded synthetic weights (oracle/synth.py formula, bit-identical)
 #include "common.h"
@@ -75,29 +76,20 @@ extern "C" int pg_image_rank(const int64_t* ids, int n, long image_id, int* rank
 // ---------------------------------------------------------------- embedding merge
 // out f32 [n][H]: text row -> embed[id] * normalizer; image row -> feat[rank] * img_scale * normalizer;
 // pad row -> 0.  rank may be null (then computed by scanning ids[0..row), meant for n <= 64).
-__global__ __launch_bounds__(256) void embed_merge_kernel(const int64_t* __restrict__ ids, const int* __restrict__ rank,
-                                                          int n, const bf16_t* __restrict__ embed, int V,
-                                                          const float* __restrict__ feat, int n_feat, int H,
-                                                          int64_t image_id, int64_t pad_id, float img_scale,
-                                                          float normalizer, float* __restrict__ out) {
-  const int row = blockIdx.x;
-  const int64_t id = ids[row];
-  float* o = out + (long)row * H;
+// one output row: pad -> zeros, image token -> feat[rank] (zeros past n_feat) * img_scale * normalizer,
+// text -> embed[clamp(id)] * normalizer; threads t, t + nt, ... of the caller each write 4 columns at a time
+__device__ __forceinline__ void embed_row(float* __restrict__ o, int64_t id, int rk, int t, int nt,
+                                          const bf16_t* __restrict__ embed, int V, const float* __restrict__ feat,
+                                          int n_feat, int H, int64_t image_id, int64_t pad_id, float img_scale,
+                                          float normalizer) {
   if (id == pad_id) {
-    for (int c = threadIdx.x * 4; c < H; c += 1024) *(f32x4*)(o + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = t * 4; c < H; c += 4 * nt) *(f32x4*)(o + c) = f32x4{0.f, 0.f, 0.f, 0.f};
     return;
   }
   if (id == image_id) {
-    int rk;
-    if (rank) {
-      rk = rank[row];
-    } else {
-      rk = 0;
-      for (int i = 0; i < row; ++i) rk += ids[i] == image_id;
-    }
     const bool ok = rk < n_feat;
     const float* f = feat + (long)(ok ? rk : 0) * H;
-    for (int c = threadIdx.x * 4; c < H; c += 1024) {
+    for (int c = t * 4; c < H; c += 4 * nt) {
       f32x4 v = ok ? *(const f32x4*)(f + c) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = (v[j] * img_scale) * normalizer;
@@ -107,7 +99,7 @@ __global__ __launch_bounds__(256) void embed_merge_kernel(const int64_t* __restr
   }
   const int64_t tid = id < 0 ? 0 : (id >= V ? V - 1 : id);
   const bf16_t* e = embed + tid * (long)H;
-  for (int c = threadIdx.x * 4; c < H; c += 1024) {
+  for (int c = t * 4; c < H; c += 4 * nt) {
     const u32x2 w = *(const u32x2*)(e + c);
     f32x4 v;
     v[0] = bf2f((bf16_t)(w[0] & 0xFFFF)) * normalizer;
@@ -116,6 +108,25 @@ __global__ __launch_bounds__(256) void embed_merge_kernel(const int64_t* __restr
     v[3] = bf2f((bf16_t)(w[1] >> 16)) * normalizer;
     *(f32x4*)(o + c) = v;
   }
+}
+
+__global__ __launch_bounds__(256) void embed_merge_kernel(const int64_t* __restrict__ ids, const int* __restrict__ rank,
+                                                          int n, const bf16_t* __restrict__ embed, int V,
+                                                          const float* __restrict__ feat, int n_feat, int H,
+                                                          int64_t image_id, int64_t pad_id, float img_scale,
+                                                          float normalizer, float* __restrict__ out) {
+  const int row = blockIdx.x;
+  const int64_t id = ids[row];
+  int rk = 0;
+  if (id == image_id) {
+    if (rank) {
+      rk = rank[row];
+    } else {
+      for (int i = 0; i < row; ++i) rk += ids[i] == image_id;
+    }
+  }
+  embed_row(out + (long)row * H, id, rk, threadIdx.x, blockDim.x, embed, V, feat, n_feat, H, image_id, pad_id,
+            img_scale, normalizer);
 }
 
 extern "C" int pg_embed_merge(const int64_t* ids, const int* rank, int n, const void* embed, int V, const float* feat,
@@ -253,6 +264,57 @@ __global__ __launch_bounds__(1024) void argmax_final_kernel(const float* __restr
   }
 }
 
+// argmax_final_kernel, then the next decode step's input rows: res[b] = embedding of the winner of row b,
+// exactly as pg_embed_merge(out_ids, rank = nullptr, ...) would write them (image-token rank = count of
+// earlier rows whose winner is the image token).  Saves the step's leading embed launch.
+#define AM_EMB_MAX_B 1024
+struct AmEmbArgs {
+  const bf16_t* embed;
+  int V, n_feat, H;
+  const float* feat;
+  int64_t image_id, pad_id;
+  float img_scale, normalizer;
+  float* res;
+};
+__global__ __launch_bounds__(1024) void argmax_final_embed_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                                                  int B, int64_t* __restrict__ out_ids,
+                                                                  int64_t* __restrict__ hist, int hist_rows,
+                                                                  int* __restrict__ step, int* __restrict__ pos,
+                                                                  int* __restrict__ kv_len, AmEmbArgs ea) {
+  __shared__ int win[AM_EMB_MAX_B];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int st = step ? *step : 0;
+  for (int b = wave; b < B; b += nw) {
+    float bv = pv[b * AM_CHUNKS + lane];
+    int bi = pi[b * AM_CHUNKS + lane];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float ov = __shfl_xor(bv, o, 64);
+      int oi = __shfl_xor(bi, o, 64);
+      am_better(bv, bi, ov, oi);
+    }
+    if (lane == 0) {
+      win[b] = bi;
+      out_ids[b] = bi;
+      if (hist && st < hist_rows) hist[(long)st * B + b] = bi;
+      if (pos) pos[b] += 1;
+    }
+  }
+  __syncthreads();                             // every wave has read *step and every winner is in LDS
+  if (threadIdx.x == 0) {
+    if (kv_len) *kv_len += 1;
+    if (step) *step = st + 1;
+  }
+  for (int b = wave; b < B; b += nw) {
+    const int64_t id = win[b];
+    int rk = 0;
+    if (id == ea.image_id)
+      for (int i = 0; i < b; ++i) rk += win[i] == ea.image_id;
+    embed_row(ea.res + (long)b * ea.H, id, rk, lane, 64, ea.embed, ea.V, ea.feat, ea.n_feat, ea.H, ea.image_id,
+              ea.pad_id, ea.img_scale, ea.normalizer);
+  }
+}
+
 static inline int am_waves(int B) { return B < 1 ? 1 : (B > 16 ? 16 : B); }
 
 // vocabulary-parallel greedy (tensor parallelism): the local (max, first index + vocab_offset) per row,
@@ -320,6 +382,24 @@ extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* works
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
   hipLaunchKernelGGL(argmax_final_kernel, dim3(1), dim3(64 * am_waves(B)), 0, stream, pv, pi, B, out_ids, hist, hist_rows, step, pos,
                      kv_len);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
+// pg_argmax + the next step's embedding rows (see argmax_final_embed_kernel); workspace as pg_argmax
+extern "C" int pg_argmax_embed(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
+                               int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, const void* embed,
+                               int V_embed, const float* feat, int n_feat, int H, long image_id, long pad_id,
+                               float img_scale, float normalizer, float* res, hipStream_t stream) {
+  PG_REQUIRE(B > 0 && B <= AM_EMB_MAX_B && V > 0 && ld % 4 == 0 && (hist == nullptr || hist_rows > 0));
+  PG_REQUIRE(embed != nullptr && res != nullptr && V_embed > 0 && H > 0 && H % 4 == 0 && (n_feat == 0 || feat));
+  float* pv = (float*)workspace;
+  int* pi = (int*)(pv + B * AM_CHUNKS);
+  const AmEmbArgs ea{(const bf16_t*)embed, V_embed, n_feat, H, feat, (int64_t)image_id, (int64_t)pad_id,
+                     img_scale, normalizer, res};
+  hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
+  hipLaunchKernelGGL(argmax_final_embed_kernel, dim3(1), dim3(64 * am_waves(B)), 0, stream, pv, pi, B, out_ids, hist,
+                     hist_rows, step, pos, kv_len, ea);
   PG_LAUNCH_CHECK();
   return 0;
 }

@@ -54,6 +54,8 @@ SIGNATURES = {
     "pg_image_rank": [vp, i32, i64, vp, vp],
     "pg_embed_merge": [vp, vp, i32, vp, i32, vp, i32, i32, i64, i64, f32, f32, vp, vp],
     "pg_argmax": [vp, i64, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp],
+    "pg_argmax_embed": [vp, i64, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32, vp, i32, i32, i64, i64, f32, f32, vp,
+                        vp],
     "pg_argmax_pairs": [vp, i64, i32, i32, i32, vp, vp, vp],
     "pg_argmax_merge": [vp, i32, i32, vp, vp, i32, vp, vp, vp, vp],
     "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp],

@@ -94,6 +94,9 @@ class PaliGemmaEngine:
     MLP_BLOCK = os.environ.get("PG_MLP_BLOCK", "0") == "1"
     # B = 1: gate/up + down as one persistent loader / consumer launch (pg_decode_mlp_engine, csrc/decode_engine.hip)
     MLP_ENGINE = os.environ.get("PG_MLP_ENGINE", "0") == "1"
+    # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
+    # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
+    CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -384,8 +387,16 @@ class PaliGemmaEngine:
         return g.view(rows, w.vocab) if vlp == vl else g[:, :, :vl].reshape(rows, w.vocab)
 
     # ------------------------------------------------------------------ decode step (graph-capturable)
-    def decode_state(self, B: int, cache: KVStore, positions_next: torch.Tensor, max_steps: int):
-        """Device-resident decode state: ids, positions, kv length, step counter, token history."""
+    def _chain_ok(self, sampler) -> bool:
+        return self.CHAIN_EMBED and self.tp == 1 and sampler is not None and not sampler.get("do_sample")
+
+    def decode_state(self, B: int, cache: KVStore, positions_next: torch.Tensor, max_steps: int, sampler=None):
+        """Device-resident decode state: ids, positions, kv length, step counter, token history.
+
+        With the loop's sampler given (generate / bench) and greedy single-rank decoding, the state is
+        *chained*: every sample() also writes the embedding of the sampled ids into the decode input buffer,
+        and decode_step skips its embed launch.  A caller that writes st["ids"] itself (teacher forcing)
+        builds the state without a sampler."""
         st = {
             "ids": torch.zeros(B, dtype=torch.int64, device=self.device),
             "pos": positions_next.to(device=self.device, dtype=torch.int32).reshape(B).contiguous().clone(),
@@ -393,6 +404,7 @@ class PaliGemmaEngine:
             "step": torch.zeros(1, dtype=torch.int32, device=self.device),
             "hist": torch.zeros(max_steps + 1, B, dtype=torch.int64, device=self.device),
             "ws": torch.empty(B * 64 * 2, dtype=torch.float32, device=self.device),
+            "chain": self._chain_ok(sampler),
         }
         return st
 
@@ -420,9 +432,11 @@ class PaliGemmaEngine:
         dt = (hd + 15) // 16 * 16
         part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
         part_ml = self._buf("d_pml", (B * nkv * nsplit * 16 * 2,), torch.float32)
-        ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, res_a,
-                        image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
-                        normalizer=float(w.hidden ** 0.5))
+        chain = bool(st.get("chain")) and self._chain_ok(sampler)
+        if not chain:                               # chained: the previous sample() wrote res_a already
+            ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, res_a,
+                            image_id=self.image_token_id, pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
+                            normalizer=float(w.hidden ** 0.5))
         ns = 0
         fin = self.tp == 1 and self.USE_FIN and (B <= self.FUSE_MAX_B or self.FIN_MIN_B <= B <= 16) and \
             not self._fp8_rows(B)
@@ -438,7 +452,7 @@ class PaliGemmaEngine:
             ops.gemm_fused(xq, w.lm_w, logits, fa, epi=ops.EPI_F32 | w.wflag, M=B, bias=w.lm_bias)
             logits = logits[:, :w.vocab]
             if sampler is not None:
-                self.sample(logits, st, sampler, advance=True)
+                self.sample(logits, st, sampler, advance=True, feats=feats)
             return logits
         for i, Lw in enumerate(w.tl if B <= self.FUSE_MAX_B else ()):      # (TP / USE_FIN off, B <= FUSE_MAX_B)
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
@@ -477,7 +491,7 @@ class PaliGemmaEngine:
             return loc
         logits = self.lm_head(xn, B, name="d_logits")
         if sampler is not None:
-            self.sample(logits, st, sampler, advance=True)
+            self.sample(logits, st, sampler, advance=True, feats=feats)
         return logits
 
     def check(self):
@@ -671,11 +685,21 @@ class PaliGemmaEngine:
             ns = sd
         return ns
 
-    def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool):
+    def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool,
+               feats: Optional[torch.Tensor] = None):
+        """Next ids from logits [B][V] (greedy or top-p); advance=True also moves pos / kv_len on.  A chained
+        state (decode_state) also gets the next step's input rows: pass the request's image features."""
         kw = dict(hist=st["hist"], step=st["step"])
         if advance:
             kw.update(pos=st["pos"], kv_len=st["kv_len"])
-        if sampler.get("do_sample"):
+        if st.get("chain") and self._chain_ok(sampler):
+            w = self.w
+            B = st["ids"].numel()
+            ops.argmax_embed(logits, st["ids"], st["ws"], w.embed, feats, feats.shape[0] if feats is not None else 0,
+                             self._buf("d_res_a", (B, w.hidden), torch.float32), image_id=self.image_token_id,
+                             pad_id=self.pad_id, img_scale=float(w.proj_dim ** -0.5),
+                             normalizer=float(w.hidden ** 0.5), **kw)
+        elif sampler.get("do_sample"):
             ops.topp_sample(logits, st["ids"], sampler["uniforms"], temperature=sampler["temperature"],
                             top_p=sampler["top_p"], **kw)
         else:
@@ -712,13 +736,13 @@ class PaliGemmaEngine:
         if check_every is None:
             check_every = 1 if B == 1 else 8
         cache, feats, logits, nxt = self.prefill_request(input_ids, pixel_values, attention_mask, max_new_tokens)
-        st = self.decode_state(B, cache, nxt, max_new_tokens)
         sampler = dict(do_sample=do_sample, temperature=temperature, top_p=top_p)
+        st = self.decode_state(B, cache, nxt, max_new_tokens, sampler=sampler)
         if do_sample:
             if uniforms is None:
                 uniforms = torch.rand(max_new_tokens + 1, B)
             sampler["uniforms"] = uniforms.to(device=self.device, dtype=torch.float32).contiguous()
-        self.sample(logits, st, sampler, advance=False)                  # token 1 from the prefill logits
+        self.sample(logits, st, sampler, advance=False, feats=feats)     # token 1 from the prefill logits
         n = 1
         step_fn = None
         if use_graph and self.comm.capturable:
@@ -764,6 +788,7 @@ class PaliGemmaEngine:
         # warm-up pass to allocate every workspace outside capture, then undo its state advance
         snap = {k: st[k].clone() for k in ("ids", "pos", "kv_len", "step")}
         hist0 = st["hist"].clone()
+        res0 = self._ws["d_res_a"][: st["ids"].numel() * self.w.hidden].clone() if st.get("chain") else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -773,6 +798,8 @@ class PaliGemmaEngine:
         for k, v in snap.items():
             st[k].copy_(v)
         st["hist"].copy_(hist0)
+        if res0 is not None:                        # the chained input rows the warm-up step overwrote
+            self._ws["d_res_a"][: res0.numel()].copy_(res0)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.decode_step(st, cache, feats, sampler)

@@ -318,6 +318,19 @@ def argmax(logits, out_ids, workspace, *, hist=None, step=None, pos=None, kv_len
               _p(step), _p(pos), _p(kv_len), _s())
 
 
+def argmax_embed(logits, out_ids, workspace, embed, feat, n_feat, res, *, image_id, pad_id, img_scale, normalizer,
+                 hist=None, step=None, pos=None, kv_len=None):
+    """argmax + the next step's input rows res[b] = embed_merge(winner_b) (one launch fewer per decode step)."""
+    _chk(logits, torch.float32, "logits")
+    _chk(res, torch.float32, "res")
+    B, V = logits.shape
+    Ve, H = embed.shape
+    assert res.is_contiguous() and res.numel() >= B * H
+    _lib.call("pg_argmax_embed", _p(logits), logits.stride(0), B, V, _p(workspace), _p(out_ids), _p(hist),
+              _rows(hist, B), _p(step), _p(pos), _p(kv_len), _p(embed), Ve, _p(feat), int(n_feat), H, int(image_id),
+              int(pad_id), float(img_scale), float(normalizer), _p(res), _s())
+
+
 def argmax_pairs(logits, workspace, pairs, *, vocab_offset: int):
     _chk(logits, torch.float32, "logits")
     B, V = logits.shape

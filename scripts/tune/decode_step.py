@@ -46,9 +46,10 @@ ids, px = bench.synthetic_inputs(cfg, B, [2, 651, 4906, 603, 476, 2121, 576, 108
 ids, px = ids.cuda(), px.cuda()
 T = a.steps + 1
 cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), T + 8)
-st = eng.decode_state(B, cache, nxt, T + 8)
-eng.sample(logits, st, dict(do_sample=False), advance=False)
-replay = eng._graph_step(st, cache, feats, dict(do_sample=False))
+sampler = dict(do_sample=False)
+st = eng.decode_state(B, cache, nxt, T + 8, sampler=sampler)      # chained unless PG_CHAIN_EMBED=0
+eng.sample(logits, st, sampler, advance=False, feats=feats)
+replay = eng._graph_step(st, cache, feats, sampler)
 snap = {k: st[k].clone() for k in ("ids", "pos", "kv_len", "step")}
 times = []
 for rnd in range(5):

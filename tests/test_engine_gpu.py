@@ -63,6 +63,27 @@ def test_tiny_greedy_matches_reference_loop(tiny, golden):
         assert out[0].tolist() == g["greedy_ids"].tolist()
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_chained_embed_generation_matches_unchained(tiny, golden, B):
+    """Chained greedy decode (pg_argmax_embed writes the next step's input rows, no embed launch per step)
+    == the unchained loop (embed_merge at the start of every step): identical tokens, graph and eager."""
+    eng, _ = tiny
+    g = golden("tiny")
+    ids = torch.from_numpy(g["b1_input_ids"]).cuda().repeat(B, 1)
+    px = torch.from_numpy(g["b2_pixel_values"]).cuda()
+    px = torch.cat([px, px])[:B]
+    outs = []
+    try:
+        for chain in (True, False):
+            eng.CHAIN_EMBED = chain
+            for use_graph in (True, False):
+                outs.append(eng.generate(ids, px, torch.ones_like(ids), 14, stop_token=None,
+                                         use_graph=use_graph).tolist())
+    finally:
+        eng.CHAIN_EMBED = type(eng).CHAIN_EMBED
+    assert all(o == outs[0] for o in outs[1:])
+
+
 @pytest.mark.parametrize("fuse_max_b,use_fin,attn_o", [(2, True, True), (2, True, False), (2, False, False),
                                                         (0, True, False)])
 def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin, attn_o):

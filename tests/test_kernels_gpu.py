@@ -373,6 +373,47 @@ def test_argmax_first_index_and_state_advance():
     assert step.item() == 2 and kv.item() == 4 and pos.cpu().tolist() == list(range(1, B + 1))
 
 
+@pytest.mark.parametrize("B", [1, 5, 20])
+def test_argmax_embed_equals_argmax_then_embed_merge(B):
+    """pg_argmax_embed == pg_argmax followed by pg_embed_merge(rank=None) of the winners, bit-exact: ids,
+    history, state advance and the next step's rows, including pad-token and image-token winners (the image
+    rank counts earlier rows with the image token; ranks past n_feat give zero rows)."""
+    from pghip import ops
+    V, Ve, H, n_feat = 257216, 257216, 2048, 2
+    image_id, pad_id = 257152, 0
+    gen = torch.Generator().manual_seed(B)
+    x = torch.randn(B, V, generator=gen).cuda()
+    forced = {0: image_id, 1: pad_id, 2: image_id, 3: image_id, 4: 257215}
+    for b, t in forced.items():
+        if b < B:
+            x[b, t] = 99.0
+    embed = (torch.randn(Ve, H, generator=gen) * 0.05).to(torch.bfloat16).cuda()
+    feat = torch.randn(n_feat, H, generator=gen).cuda()
+    kw = dict(image_id=image_id, pad_id=pad_id, img_scale=2048 ** -0.5, normalizer=2048 ** 0.5)
+    outs = []
+    for fused in (True, False):
+        ids = torch.empty(B, dtype=torch.int64, device="cuda")
+        ws = torch.empty(B * 64 * 2, device="cuda")
+        hist = torch.zeros(3, B, dtype=torch.int64, device="cuda")
+        step = torch.tensor([1], dtype=torch.int32, device="cuda")
+        pos = torch.arange(B, dtype=torch.int32, device="cuda")
+        kv = torch.tensor([9], dtype=torch.int32, device="cuda")
+        res = torch.full((B, H), float("nan"), device="cuda")
+        st = dict(hist=hist, step=step, pos=pos, kv_len=kv)
+        if fused:
+            ops.argmax_embed(x, ids, ws, embed, feat, n_feat, res, **kw, **st)
+        else:
+            ops.argmax(x, ids, ws, **st)
+            ops.embed_merge(ids, None, embed, feat, n_feat, res, **kw)
+        outs.append([t.cpu() for t in (ids, hist, step, pos, kv, res)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ids, res = outs[0][0], outs[0][5]
+    assert ids.tolist()[: min(B, 5)] == [forced[b] for b in range(min(B, 5))]
+    if B >= 4:                                       # third image winner: rank 2 >= n_feat -> zeros
+        assert (res[3] == 0).all() and (res[1] == 0).all() and (res[0] != 0).any() and (res[2] != 0).any()
+
+
 def test_topp_matches_reference_filter(golden):
     from oracle import paligemma_oracle as O
     from pghip import ops
