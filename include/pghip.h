@@ -94,6 +94,11 @@ typedef struct PgFusedArgs {
  * 16x16x128 block-scaled MFMA with unit block scales (2x the bf16 rate).  M > 16, K % 128 == 0, lda and ldw
  * multiples of 16, no prologue, epi in {BF16, BF16_GELU_MUL, F32, QKV_ROPE}. */
 #define PG_FP8 0x200
+/* PG_TILE_M1 (bf16 tile GEMMs, 256 <= M <= 288: batch-1 prefill, 256 image rows + the prompt): all M rows
+ * in ONE row tile per 128 output columns, so each weight tile streams from HBM once (the 256x256 tiling
+ * spends a second row tile -- and a second weight read -- on the last M - 256 rows).  Measured on the
+ * pt-224 Gemma gate/up (ks 1), down (ks 16) and o (ks 8) shapes. */
+#define PG_TILE_M1 0x400
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
  * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0

@@ -26,9 +26,6 @@
 #ifndef PG_G256_STAGGER
 #define PG_G256_STAGGER 1       // gemm256: wave groups one barrier apart (MFMA of one || LDS reads of the other); +4-14%
 #endif
-#ifndef PG_SKINNY
-#define PG_SKINNY 0             // prefill GEMMs of 161..288 rows as one 256- or 288-row tile per 128 columns
-#endif
 #ifndef PG_G256_PREFETCH
 #define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
 #endif
@@ -100,6 +97,7 @@ __device__ __forceinline__ f32x4 load4_guard(const float* __restrict__ p, int n0
 }
 
 #define PG_W_FRAG 0x100   // weight layout flag OR-ed into epi (include/pghip.h)
+#define PG_TILE_M1 0x400  // one row tile of all M (256..288) rows (include/pghip.h)
 #define PG_FP8 0x200      // A and W fp8 e4m3 with row scales (PgFusedArgs a_scale / w_scale), M > 16
 
 struct EpiArgs {
@@ -1444,11 +1442,11 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // F8: A, W fp8 viewed as bf16-sized pairs (K, lda, ldw in 2-byte units: a 64-unit k-tile = 128 fp8 k)
 template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
-                        hipStream_t st) {
+                        hipStream_t st, bool m1 = false) {
   if constexpr (!F8) {
-    if (PG_SKINNY && e.M > 160 && e.M <= 288) {
-      // skinny prefill (batch 1: 256 image + a few text rows): ALL rows in one tile, so every weight tile streams
-      // once and no 256-row tile is spent on an 8-row remainder (M = 264: 2 x 256 rows in gemm256)
+    if (m1) {
+      // PG_TILE_M1 (batch-1 prefill: 256 image + a few text rows): ALL rows in one tile, so every weight tile
+      // streams once and no 256-row tile is spent on an 8-row remainder (M = 264: 2 x 256 rows in gemm256)
       const int tiles_n = (e.N + TBN - 1) / TBN;
       const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
       if (e.M <= 256)
@@ -1560,11 +1558,11 @@ static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
 // M <= 16 -> weight-streaming GEMV, else the tile GEMM; FRAG (PG_W_FRAG) only for the Gemma epilogues
 template <int EPI, bool FRAG>
 static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
-                       hipStream_t st) {
+                       hipStream_t st, bool m1 = false) {
   if (e.M <= 16)
     launch_gemv<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
   else if constexpr (EPI != PG_EPI_F32_FIN)
-    launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+    launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st, m1);
 }
 
 static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
@@ -1573,8 +1571,10 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                      const AttnArgs* att = nullptr, int att_total = 0, int* sync = nullptr) {
   const bool frag = (epi_flags & PG_W_FRAG) != 0;
   const bool fp8 = (epi_flags & PG_FP8) != 0;
+  const bool m1 = (epi_flags & PG_TILE_M1) != 0;
   const int epi = epi_flags & 0xFF;
-  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8)) == 0);
+  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8 | PG_TILE_M1)) == 0);
+  if (m1) PG_REQUIRE(!fp8 && M >= 256 && M <= 288 && (fa == nullptr || fa->pro_mode == 0));
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
@@ -1637,11 +1637,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   }
 #define PG_CASE(E)                                                                             \
   case E:                                                                                      \
-    if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream);                       \
-    else launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream);                           \
+    if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream, m1);                   \
+    else launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1);                       \
     break;
 #define PG_CASE_ROWMAJOR(E)                                                                    \
-  case E: launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream); break;
+  case E: launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1); break;
   switch (epi) {
     PG_CASE(PG_EPI_BF16)
     PG_CASE(PG_EPI_BF16_GELU_MUL)

@@ -68,6 +68,9 @@ class PaliGemmaEngine:
                               # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
     DECODE_SPLIT_DOWN = 8   # split-K of down_proj at decode (8 vs 4: -4..6 us per pt-224 step, scripts/r02/gpu_t.sh)
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
+    # keys per split at B <= FUSE_MAX_B: every o_proj workgroup merges all active splits in its prologue, so
+    # fewer, longer splits (one wave per 32 keys, merged in LDS by attn_decode_wg_kernel) cut that re-read
+    DECODE_SPLIT_KEYS_SMALL = int(os.environ.get("PG_SK_SMALL", "32"))
     # prefill GEMMs of at least this many rows read the row-major weight copies (weights.prefill_rowmajor)
     PREFILL_ROWMAJOR_MIN_M = int(os.environ.get("PG_ROWMAJOR_MIN_M", "256"))
     ROW_BLOCKS = os.environ.get("PG_ROW_BLOCKS", "1") != "0"   # ragged fp32-slab GEMMs as head + tail launches
@@ -77,6 +80,12 @@ class PaliGemmaEngine:
     # ragged-N SigLIP GEMMs as head + tail launches: measured neutral at pt-448 x16 and pt-896 x32 (the small-tile
     # tail costs what the saved round gave back; scripts/tune/run_s4_p.sh), so off
     COL_BLOCKS = os.environ.get("PG_COL_BLOCKS", "0") == "1"
+    # batch-1 prefill (256 <= rows <= 288): these Gemma linears run as ONE row tile per 128 columns (PG_TILE_M1),
+    # with this split-K -- each weight tile streams once instead of once per 256-row tile.  Per call at 264 rows
+    # (scripts/tune/skinny_bench.py, profiles/r02_skinny_gemm_*.txt): gate/up 60.8 -> 52.8 us, down 38.9 -> 33.5,
+    # o 15.2 -> 14.1.  The q|k|v / SigLIP epilogues cannot split K, so their one-tile grids would idle most CUs.
+    TILE_M1 = os.environ.get("PG_TILE_M1", "1") != "0"
+    TILE_M1_SPLIT = {"gu": 1, "down": 16, "o": 8}
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
@@ -266,12 +275,22 @@ class PaliGemmaEngine:
         fewer fp32 slabs are written and re-read by the next RMSNorm."""
         if self._fp8_rows(M):
             return ops.gemm_ksplit(M, N, K // 2)
+        m1 = self._tile_m1(M, "down" if K == self.w.inter else "o")
+        if m1:
+            return m1
         Mh = M // 256 * 256
         if self.ROW_BLOCKS and self.HEAD_KSPLIT and 0 < Mh < M:
             s = ops.gemm_ksplit(Mh, N, K)
             if self._row_head(M, N, s):
                 return s
         return ops.gemm_ksplit(M, N, K)
+
+    def _tile_m1(self, M: int, name: str) -> int:
+        """split-K of a batch-1 prefill linear run as one row tile (PG_TILE_M1), 0 when it does not apply."""
+        if (not self.TILE_M1 or self.fp8 or self.tp != 1 or not 256 <= M <= 288
+                or M < self.PREFILL_ROWMAJOR_MIN_M):
+            return 0
+        return self.TILE_M1_SPLIT.get(name, 0)
 
     def _lin(self, x: torch.Tensor, Lw: dict, name: str, out: torch.Tensor, epi: int, M: int, ksplit: int = 1,
              fa=None):
@@ -290,6 +309,8 @@ class PaliGemmaEngine:
         W, flag = Lw[name + "_w"], w.wflag
         if M >= self.PREFILL_ROWMAJOR_MIN_M and name + "_wr" in Lw:
             W, flag = Lw[name + "_wr"], 0
+            if fa is None and self._tile_m1(M, name) == ksplit:
+                return ops.gemm(x, W, out, epi=epi | ops.TILE_M1, ksplit=ksplit)
         if fa is None and epi == ops.EPI_F32 and self.ROW_BLOCKS:
             Mh = self._row_head(M, W.shape[0], ksplit)
             if Mh:
@@ -647,7 +668,7 @@ class PaliGemmaEngine:
         partials to write and merge once the batch alone fills the chip."""
         SK = self.DECODE_SPLIT_KEYS
         if B <= self.FUSE_MAX_B:
-            return SK
+            return self.DECODE_SPLIT_KEYS_SMALL
         blocks = (Smax + SK - 1) // SK
         mult = max(1, min(8, (B * blocks) // self.DECODE_SPLIT_TARGET))
         # a power of two: 2 / 4 / 8-block splits run one wave per block, merged in LDS (attn_decode_wg_kernel)

@@ -17,6 +17,7 @@ EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, E
 PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD, PRO_ATTN_INLINE = range(6)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
+TILE_M1 = 0x400  # OR into epi: all 256..288 rows in one row tile (batch-1 prefill, include/pghip.h PG_TILE_M1)
 
 
 def _p(t: Optional[torch.Tensor]):

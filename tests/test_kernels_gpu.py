@@ -136,6 +136,30 @@ def test_gemm_gelu_and_gelu_mul(M):
     assert err(out2, torch.nn.functional.gelu(A.float() @ g.float().t() + bias, approximate="tanh")) < 1e-2
 
 
+@pytest.mark.parametrize("M", [256, 264, 288])
+def test_gemm_tile_m1_batch1_prefill(M):
+    """PG_TILE_M1 (all 256..288 rows in one row tile; the batch-1 prefill Gemma gate/up, down and o) against a
+    torch fp32 matmul: the gelu*up epilogue, and fp32 split-K slabs at the engine's splits (8, 16) with a
+    ragged last k-slice; rows past M are never written."""
+    from pghip import ops
+    K, I = 2048, 640
+    A = rnd(M, K, seed=41)
+    g, u = rnd(I, K, scale=1 / math.sqrt(K), seed=42), rnd(I, K, scale=1 / math.sqrt(K), seed=43)
+    gu = torch.stack([g.view(I // 16, 16, K), u.view(I // 16, 16, K)], 1).reshape(2 * I, K).contiguous()
+    out = torch.full((M + 8, I), 7.0, dtype=torch.bfloat16, device="cuda")
+    ops.gemm(A, gu, out[:M], epi=ops.EPI_BF16_GELU_MUL | ops.TILE_M1)
+    ref = torch.nn.functional.gelu(A.float() @ g.float().t(), approximate="tanh") * (A.float() @ u.float().t())
+    assert err(out[:M], ref) < 1e-2 and (out[M:] == 7.0).all()
+    for K2, s in ((2048, 8), (3072 + 64, 16)):
+        A2, W2 = rnd(M, K2, seed=44), rnd(512, K2, scale=1 / math.sqrt(K2), seed=45)
+        bias = torch.randn(512).cuda() * 0.1
+        part = torch.empty(s, M, 512, dtype=torch.float32, device="cuda")
+        ops.gemm(A2, W2, part, epi=ops.EPI_F32 | ops.TILE_M1, ksplit=s, bias=bias)
+        assert err(part.sum(0), A2.float() @ W2.float().t() + bias) < 1e-4
+    with pytest.raises(RuntimeError):                   # outside 256..288 rows the flag is refused
+        ops.gemm(A[:200], gu, out[:200], epi=ops.EPI_BF16_GELU_MUL | ops.TILE_M1)
+
+
 @pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 264])
 @pytest.mark.parametrize("N,K", [(256, 128), (2048, 2048), (320, 1024)])
 def test_gemm_frag_packed_weights_bit_identical(M, N, K):
