@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 2: pg_attention takes kcap */
+int pg_abi_version(void);   /* 3: PgFusedArgs two-stream fields, pg_gateup_bank */
 
 /* Epilogues of pg_gemm */
 enum {
@@ -80,6 +80,16 @@ typedef struct PgFusedArgs {
   int slab_rows;            /* PG_EPI_F32 split-K: rows between slabs (slab z of row m at C + (z*slab_rows + m)*ldc);
                                0 = M.  Lets a GEMM be issued as row blocks that write into one [ksplit][rows][N]
                                partial tensor (C pointing at the block's first row)                            */
+  /* two-stream batch-1 decode (pghip engine; the producer and the consumer run on different streams):
+   * done_cnt   PG_EPI_F32_FIN: residual, x' and sums of squares stored write-through, then +1 per finalised tile;
+   * wait_cnt   pro_mode 7 (= pro 4, batch-1 q|k|v): weights issued first, then wait until *wait_cnt >= wait_target,
+   *            x' and ss_in read with agent-scope loads; exit_cnt: the grid's last workgroup past the wait re-arms
+   *            *wait_cnt and *exit_cnt to 0; err: set to 1 if the wait gave up (0.2 s)                        */
+  int* done_cnt;
+  const int* wait_cnt;
+  int wait_target;
+  int* exit_cnt;
+  int* err;
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -177,6 +187,21 @@ int pg_decode_mlp_engine(const void* xq, const float* ss_in, int ss_n, float eps
 /* Diagnostics: every later pg_decode_mlp_engine launch records per CU [start, h published, h half gathered,
  * down done, end, -, -, -] (100 MHz wall clock, u64) into buf [256][8]; null turns it off. */
 int pg_decode_mlp_engine_stamps(void* buf);
+
+/* Batch-1 decode gate/up GEMV that banks half its weights on-chip before its input exists (csrc/decode_bank.hip):
+ * launched on a second stream beside the q|k|v -> attention -> o_proj chain, one workgroup per CU loads tile pair
+ * 0 of its four into registers and pair 1 into LDS, waits until *wait_cnt >= wait_target (the o_proj F32_FIN
+ * producer's done_cnt), then computes h = gelu(rstd*gate)*(rstd*up) bit-identically to
+ * pg_gemm_fused(gate/up, PG_EPI_BF16_GELU_MUL | PG_W_FRAG, pro_mode 4) while pairs 2 and 3 stream.  Replaces
+ * GemmaMLP gate_proj/up_proj + gelu*up (modeling_gemma.py:210-218) at batch 1.  wait_cnt / exit_cnt: zeroed
+ * once, self re-arming.  hipErrorNotSupported unless M == 1, H == 2048, I == 16384. */
+int pg_gateup_bank(const void* xq, const float* ss_in, int ss_n, float eps, const void* wgu, void* h,
+                   const int* wait_cnt, int wait_target, int* exit_cnt, int* err, int M, int H, int I,
+                   hipStream_t stream);
+int pg_gateup_bank_stamps(void* buf);
+/* Diagnostics: every later GEMV launch (M <= 16) k records its workgroups' start / end wall clock (100 MHz) into
+ * slot k % 128 of buf [128][2048][2] u64; null turns it off. */
+int pg_gemv_stamps(void* buf);
 
 /* Diagnostics: every later pg_decode_mlp_block launch records per workgroup [start, h published, h slice ready,
  * end] (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */

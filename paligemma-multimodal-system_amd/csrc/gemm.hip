@@ -85,6 +85,15 @@ struct PgFusedArgs {
   const float* a_scale;      // [M]
   const float* w_scale;      // [N] (in W's row order, e.g. the packed q|k|v or interleaved gate/up rows)
   int slab_rows;             // PG_EPI_F32 split-K: rows between slabs (0 = M); lets a GEMM run as row blocks
+  // two-stream decode (pghip engine, batch 1): a PG_EPI_F32_FIN producer stores its finalised residual / x' / sums
+  // of squares write-through and adds 1 per finalised tile to done_cnt; a pro_mode 7 consumer (pro 4 whose input
+  // comes from a launch on ANOTHER stream) issues its weights, waits until *wait_cnt >= wait_target, then reads x'
+  // and ss_in with agent-scope loads; the workgroup whose exit_cnt add is the grid's last re-arms both counters
+  int* done_cnt;
+  const int* wait_cnt;
+  int wait_target;
+  int* exit_cnt;
+  int* err;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -1081,32 +1090,41 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   const int Kr = per_z * CH;                    // K range of this split (LDS row length)
   // rows past M read row M-1 (their outputs are never stored): the x loads are unconditional, so the compiler
   // has no select or branch to resolve and no reason to wait for them before issuing the rest of the stream
-  const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : M - 1) * lda : nullptr;
+  const bf16_t* xrow = (PRO == 0 || PRO == 4 || PRO == 7) ? A + (size_t)(xvalid ? r : M - 1) * lda : nullptr;
   // PRO 4 (M <= 2): wave 0 loads the producer's per-tile sums of squares before the weight stream (all
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
   // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
   // own row, so the row total is a reduction over the 4 lane groups
   // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- use the same 16-entry layout as the
   // two-tile form)
-  constexpr bool SS16 = PRO == 4 && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
+  constexpr bool SS16 = (PRO == 4 || PRO == 7) && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
   constexpr int SSL = SS16 ? 16 : 4;
   float ssv[SSL];
 #pragma unroll
   for (int k = 0; k < SSL; ++k) ssv[k] = 0.f;
-  if constexpr (PRO == 4) {
+  // pro 7: the same entries, read with agent-scope loads after the wait (the producer ran on another stream)
+  auto ldss = [&](const float* p) -> float {
+    if constexpr (PRO == 7)
+      return __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned*)p, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT));
+    else
+      return *p;
+  };
+  auto load_ss = [&]() {
     if (wave == 0) {
       if (SS16 && M > 2) {
         const int rr = min(r, M - 1);
 #pragma unroll
-        for (int k = 0; k < SSL; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(g + 4 * k, e.f.ss_n - 1)];
+        for (int k = 0; k < SSL; ++k) ssv[k] = ldss(e.f.ss_in + (size_t)rr * e.f.ss_ld + min(g + 4 * k, e.f.ss_n - 1));
       } else {
         const int lpr = M == 1 ? 64 : 32;
         const int rr = min(lane / lpr, M - 1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(lane % lpr + k * lpr, e.f.ss_n - 1)];
+        for (int k = 0; k < 4; ++k) ssv[k] = ldss(e.f.ss_in + (size_t)rr * e.f.ss_ld + min(lane % lpr + k * lpr, e.f.ss_n - 1));
       }
     }
-  }
+  };
+  if constexpr (PRO == 4) load_ss();
   const bf16_t* xlds = xs + (xvalid ? r : M - 1) * (Kr + XPAD);
   // PG_EPI_QKV_ROPE: the epilogue's rotary positions and cache slot load before the weight stream, its cos/sin
   // right after the first chunks are issued, so the epilogue starts without a dependent round trip
@@ -1160,7 +1178,16 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   };
   auto loadx = [&](int j, u32x4 (&xv)[U]) {
     const int koff = (wave + j * 4) * CH + LANE_OFF;      // offset inside this split
-    if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
+    if constexpr (PRO == 7) {
+      typedef __attribute__((address_space(1))) unsigned long long gx64;
+#pragma unroll
+      for (int s = 0; s < U; ++s) {
+        const gx64* px = (const gx64*)(xrow + c0 * CH + koff + S_STRIDE * s);
+        const unsigned long long lo = __hip_atomic_load(px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long hi = __hip_atomic_load(px + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xv[s] = u32x4{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+      }
+    } else if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
         xv[s] = *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s);
@@ -1169,7 +1196,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       for (int s = 0; s < U; ++s) xv[s] = *(const u32x4*)(xlds + koff + S_STRIDE * s);
     }
   };
-  constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
+  constexpr bool STAGED = (PRO != 0 && PRO != 4 && PRO != 7) || PG_GEMV_XLDS;   // x built in LDS by a prologue
   // weights issued before the prologue, except by the attention workgroups of pro_mode 5 (their publish
   // drains vmcnt: the attention result, not their weights, is on everyone's critical path)
   const bool prew = STAGED && PG_GEMV_PREW && !(PRO == 5 && gi.by * gi.nx + gi.bx < e.att_wgs);
@@ -1186,7 +1213,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   for (int d = 0; d < DEPTH; ++d)
     if (CPW > 0 ? d < CPW : d < mine) {
       if (!prew) loadw(d, wb[d]);
-      loadx(d, xb[d]);
+      if constexpr (PRO != 7) loadx(d, xb[d]);
     }
   // PG_EPI_F32_FIN: the residual rows and norm weights the tile's last-arriving split finalises are loaded now
   // (nothing else writes them in this launch), so the reducer's only round trip is the slab read
@@ -1211,6 +1238,29 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       rope_cs[t] = *(const f32x4*)(e.f.cos_t + off);
       rope_sn[t] = *(const f32x4*)(e.f.sin_t + off);
     }
+  }
+  if constexpr (PRO == 7) {
+    // the weights (and the epilogue's own operands) are in flight: wait for the producer on the other stream
+    if (threadIdx.x == 0) {
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load(e.f.wait_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.f.wait_target) {
+        if (wall_clock64() - t0 > PG_BLOCK_TIMEOUT_TICKS) {
+          __hip_atomic_store(e.f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (__hip_atomic_fetch_add(e.f.exit_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+          (int)(gridDim.x * gridDim.y) - 1) {
+        __hip_atomic_store((int*)e.f.wait_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(e.f.exit_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_barrier" ::: "memory");     // (no fence: the weight loads stay in flight)
+    load_ss();
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+      if (CPW > 0 ? d < CPW : d < mine) loadx(d, xb[d]);
   }
   if constexpr (CPW > 0) {
     // sched_barrier: the scheduler may not sink the ring's loads below later MFMAs (it otherwise trades the
@@ -1268,7 +1318,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] *= rs;
   }
-  if constexpr (PRO == 4) {
+  if constexpr (PRO == 4 || PRO == 7) {
     // the raw per-tile entries were loaded with clamped indices (no select before the weight stream): mask here
     float ss = 0.f;
     if (SS16 && M > 2) {
@@ -1299,15 +1349,44 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     // The reducer reads the slabs with sc1 loads (bypass its L1/L2), so no acquire fence either.
     const PgFusedArgs& f = e.f;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
+    // done_cnt (two-stream decode): everything a consumer on the other stream reads is stored write-through
     auto finish = [&](int t, int n0, f32x4 v, float& ssl) {   // v = the finalised residual of (m, n0..n0+3)
-      *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
+      if (f.done_cnt) {
+        gu64* rp = (gu64*)(f.fin_resid + (size_t)m * e.N + n0);
+        __hip_atomic_store(rp, __builtin_bit_cast(unsigned long long, f32x2{v[0], v[1]}), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(rp + 1, __builtin_bit_cast(unsigned long long, f32x2{v[2], v[3]}), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
+      }
       ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
       if (f.fin_x) {
         const f32x4 w = fin_w[t];
         u32x2 pk;
         pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
         pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
-        *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
+        if (f.done_cnt)
+          __hip_atomic_store((gu64*)(f.fin_x + (size_t)m * e.N + n0), __builtin_bit_cast(unsigned long long, pk),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
+      }
+    };
+    auto put_ss = [&](float ssl) {
+      if (g == 0 && m < M) {
+        float* sp = f.ss_out + (size_t)m * f.ss_ld + gi.bx;
+        if (f.done_cnt)
+          __hip_atomic_store((__attribute__((address_space(1))) unsigned*)sp, __float_as_uint(ssl), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *sp = ssl;
+      }
+    };
+    auto arrive = [&]() {   // after this wave's (the only storing wave's) stores have drained
+      if (f.done_cnt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(f.done_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
     if (gi.ny == 1) {
@@ -1324,7 +1403,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       }
       ssl += __shfl_xor(ssl, 16, 64);
       ssl += __shfl_xor(ssl, 32, 64);
-      if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
+      put_ss(ssl);
+      arrive();
       return;
     }
 #pragma unroll
@@ -1373,8 +1453,9 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     }
     ssl += __shfl_xor(ssl, 16, 64);
     ssl += __shfl_xor(ssl, 32, 64);
-    if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
+    put_ss(ssl);
     if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    arrive();
     return;
   }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
@@ -1399,8 +1480,22 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG, int CPW = 0>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
                                                    const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
+  // diagnostics (pg_gemv_stamps): start / end of workgroup blockIdx.y * gridDim.x + blockIdx.x (< 2048), thread 0
+  const int sid = blockIdx.y * gridDim.x + blockIdx.x;
+  if (e.stamps && threadIdx.x == 0 && sid < 2048) e.stamps[2 * sid] = wall_clock64();
   gemv_body<EPI, NT, U, DEPTH, PRO, FRAG, CPW>(A, lda, W, ldw, K, e,
                                                GemvIdx{(int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y});
+  if (e.stamps && threadIdx.x == 0 && sid < 2048) e.stamps[2 * sid + 1] = wall_clock64();
+}
+
+// Diagnostics: with a buffer set, every later GEMV launch (M <= 16) k records its workgroups' start / end wall clock
+// (100 MHz) into slot k % 128 of buf [128][2048][2] u64 (captured launches keep their slot); null turns it off
+static unsigned long long* g_gemv_stamps = nullptr;
+static unsigned g_gemv_launch = 0;
+extern "C" int pg_gemv_stamps(void* buf) {
+  g_gemv_stamps = (unsigned long long*)buf;
+  g_gemv_launch = 0;
+  return 0;
 }
 
 // --------------------------------------------------------------------------------------
@@ -1507,7 +1602,7 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   const int CH = 64;                                   // U = 2
   const int per_z = (K / CH + ksplit - 1) / ksplit;
   size_t lds = 0;
-  if ((PRO != 0 && PRO != 4) || PG_GEMV_XLDS) {
+  if ((PRO != 0 && PRO != 4 && PRO != 7) || PG_GEMV_XLDS) {
     lds = (size_t)e.M * (per_z * CH + XPAD) * 2;
     lds = (lds + 15) & ~(size_t)15;
     if (PRO == 1) lds += 64 * sizeof(float);
@@ -1548,6 +1643,9 @@ static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
     case 2: launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 3: launch_gemv_pro<EPI, 3, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 4: launch_gemv_pro<EPI, 4, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
+    case 7:
+      if constexpr (EPI == PG_EPI_QKV_ROPE && FRAG) launch_gemv_pro<EPI, 7, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+      break;
     case 5:
       if constexpr (EPI == PG_EPI_F32_FIN || EPI == PG_EPI_F32) launch_gemv_pro<EPI, 5, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
       break;
@@ -1583,6 +1681,8 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
+  if (g_gemv_stamps && M <= 16 && f.pro_mode != 5)
+    e.stamps = g_gemv_stamps + (size_t)(g_gemv_launch++ % 128) * 2048 * 2;
   if (f.pro_mode == 5) {
     PG_REQUIRE(att != nullptr && sync != nullptr && att_total > 0 && f.asplit <= 16 && M <= 2 &&
                (epi == PG_EPI_F32_FIN || epi == PG_EPI_F32) && att->D <= 256);
@@ -1592,11 +1692,15 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
     e.sync = sync;
     PG_REQUIRE(e.att_wgs <= ((N + 15) / 16) * ksplit);            // attention roles are a prefix of the grid
   } else {
-    PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 4);
+    PG_REQUIRE((f.pro_mode >= 0 && f.pro_mode <= 4) || f.pro_mode == 7);
   }
-  if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
+  // pro 7: the batch-1 decode q|k|v of the two-stream schedule (every weight chunk issued before the wait)
+  if (f.pro_mode == 7)
+    PG_REQUIRE(M == 1 && epi == PG_EPI_QKV_ROPE && frag && ksplit == 1 && K == 2048 && f.wait_cnt && f.exit_cnt &&
+               f.err && f.wait_target > 0);
+  if (f.pro_mode == 0 || f.pro_mode == 4 || f.pro_mode == 7) PG_REQUIRE(A != nullptr && lda >= K);
   // (M > 4 runs two 16-row tiles per workgroup: the per-row entries are loaded 16 per lane)
-  if (f.pro_mode == 4) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
+  if (f.pro_mode == 4 || f.pro_mode == 7) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
                                   ((M <= 2 && f.ss_n <= 256 && (M == 1 || f.ss_n <= 128)) ||
                                    (M > 4 && M <= 16 && f.ss_n <= 64)));
   if (f.pro_mode != 0) PG_REQUIRE(M <= 16);

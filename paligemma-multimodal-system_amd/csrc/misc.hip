@@ -578,7 +578,7 @@ extern "C" int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, f
   return 0;
 }
 
-extern "C" int pg_abi_version(void) { return 2; }
+extern "C" int pg_abi_version(void) { return 3; }
 
 // ---------------------------------------------------------------- image pre-processing (processing_paligemma.py:13-73)
 // PIL BICUBIC resize of an RGB uint8 image (Pillow Resample.c, 22-bit fixed point, coefficient tables from

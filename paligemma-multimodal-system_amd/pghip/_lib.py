@@ -26,7 +26,8 @@ class PgFusedArgs(C.Structure):
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
                 ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
-                ("slab_rows", C.c_int)]
+                ("slab_rows", C.c_int), ("done_cnt", C.c_void_p), ("wait_cnt", C.c_void_p),
+                ("wait_target", C.c_int), ("exit_cnt", C.c_void_p), ("err", C.c_void_p)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -42,6 +43,9 @@ SIGNATURES = {
     "pg_decode_mlp_stamps": [vp],
     "pg_decode_mlp_engine": [vp, vp, i32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
     "pg_decode_mlp_engine_stamps": [vp],
+    "pg_gateup_bank": [vp, vp, i32, f32, vp, vp, vp, i32, vp, vp, i32, i32, i32, vp],
+    "pg_gateup_bank_stamps": [vp],
+    "pg_gemv_stamps": [vp],
     "pg_decode_mlp_block": [vp, vp, i32, i32, f32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
                             vp],
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],

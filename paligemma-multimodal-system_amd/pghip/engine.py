@@ -106,6 +106,17 @@ class PaliGemmaEngine:
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
+    # B = 1, single rank: two-stream decode layers (_decode_layers_bank) -- the gate/up GEMV (pg_gateup_bank) and
+    # the down projection run on a side stream, each gate/up launched when the previous down ends so it loads half
+    # its weights on-chip while the q|k|v -> attention -> o_proj chain runs; the q|k|v GEMV likewise issues its
+    # weights before the down projection's hand-off (pro_mode 7).  The streams meet through done counters only.
+    DECODE_BANK = os.environ.get("PG_DECODE_BANK", "0") == "1"
+    # keys per attention split in that mode: 64 = two 32-key waves merged in LDS (attn_decode_wg_kernel, 236
+    # registers), so an attention wave fits on a SIMD beside a resident gate/up wave
+    BANK_SPLIT_KEYS = int(os.environ.get("PG_BANK_SK", "64"))
+    # tuning A/B: 0 = the next layer's q|k|v waits for the down projection through a stream dependency (a per-layer
+    # cross-queue edge) instead of in-kernel (pro_mode 7)
+    BANK_QKV_WAIT = os.environ.get("PG_BANK_QKV_WAIT", "1") != "0"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -133,6 +144,8 @@ class PaliGemmaEngine:
         self._block_ok = True      # pg_decode_attn_block accepted by this device (else the three-launch form)
         self._mlp_ok = True        # pg_decode_mlp_block accepted by this device (else the two-launch form)
         self._engine_ok = True     # pg_decode_mlp_engine accepted by this device
+        self._bank_ok = True       # pg_gateup_bank accepted by this device
+        self._side = None          # side stream of the two-stream decode layers
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name, shape, dtype):
@@ -526,6 +539,9 @@ class PaliGemmaEngine:
         sync = self._ws.get("d_mlp_sync")
         if sync is not None and int(sync[576].item()):
             raise RuntimeError("pg_decode_mlp_block: an in-launch wait timed out")
+        err = self._ws.get("d_bank_err")
+        if err is not None and int(err[0].item()):
+            raise RuntimeError("two-stream decode: a cross-stream wait timed out")
 
     def _split_o(self, B: int) -> int:
         if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
@@ -565,6 +581,9 @@ class PaliGemmaEngine:
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
         SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
+        if self._bank_on(B) and SK == self.BANK_SPLIT_KEYS:
+            return self._decode_layers_bank(st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t,
+                                            SK, xq, ss_o, ss_d, cnt, tiles, n_ss)
         block = (self.FUSE_BLOCK and merge_in_gemv and self._block_ok and w.frag and hd == 256 and SK == 32 and
                  nsplit <= 16 and cache.Smax % 32 == 0)
         if block:
@@ -632,6 +651,72 @@ class PaliGemmaEngine:
             self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
         return xq, ss_d, tiles, n_ss
 
+    def _bank_on(self, B: int) -> bool:
+        w = self.w
+        return (self.DECODE_BANK and self._bank_ok and B == 1 and self.tp == 1 and self.USE_FIN and w.frag and
+                not self.fp8 and w.hidden == 2048 and w.inter == 16384 and not self.FUSE_BLOCK and
+                not self.MLP_ENGINE and not self.MLP_BLOCK and not self.FUSE_ATTN_O)
+
+    def _decode_layers_bank(self, st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t, SK, xq,
+                            ss_o, ss_d, cnt, tiles, n_ss):
+        """_decode_layers_fin at B = 1 on two streams.  Main stream: q|k|v -> attention -> o_proj (F32_FIN, counts
+        its finalised tiles into done[l][0]).  Side stream: pg_gateup_bank (issued when the previous layer's down
+        ends: half its weights load while the main stream's chain runs; waits for done[l][0]) -> down (F32_FIN,
+        counts into done[l][2]).  The next layer's q|k|v is launched right after this o_proj, issues all its weights
+        and waits for done[l][2] (pro_mode 7).  Every cross-stream value is stored write-through before the count
+        and read with agent-scope loads; the counters re-arm themselves.  One fork at the start of the step and one
+        join at the end are the only stream dependencies, so the captured graph has no per-layer cross-queue edge.
+        Bit-identical to _decode_layers_fin with the same attention split."""
+        w = self.w
+        H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
+        kvd = nkv * hd
+        so, sd = self._split_o(1), self.split_down
+        nl = len(w.tl)
+        # per layer: [0] o_proj tiles done, [1] gate/up workgroups past the wait, [2] down tiles done, [3] q|k|v
+        # workgroups past the wait -- each on a 256-byte line of its own
+        done = self._zeros("d_bank_cnt", (nl, 4, 64), torch.int32)
+        err = self._zeros("d_bank_err", (64,), torch.int32)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        main, side = torch.cuda.current_stream(), self._side
+        side.wait_stream(main)
+        for i, Lw in enumerate(w.tl):
+            rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
+                        slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
+                        q_heads=nh, kv_heads=nkv)
+            if i == 0:      # the embedding rows are final (same stream): plain RMSNorm prologue
+                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
+                                    **rope)
+                ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
+            elif self.BANK_QKV_WAIT:
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD_WAIT, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6,
+                                    wait_cnt=done[i - 1, 2], wait_target=tiles, exit_cnt=done[i - 1, 3], err=err,
+                                    **rope)
+                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
+            else:
+                main.wait_stream(side)
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
+                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
+            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=1, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
+                          part_ml=part_ml, kcap=cache.Smax)
+            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
+                                akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
+                                norm_w=Lw["post_w"], done_cnt=done[i, 0])
+            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=1, ksplit=so)
+            nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
+            with torch.cuda.stream(side):
+                if not ops.gateup_bank(xq, ss_o, Lw["gu_w"], h, done[i, 0], done[i, 1], err, wait_target=tiles):
+                    raise RuntimeError("pg_gateup_bank refused the Gemma-2B batch-1 shape")
+                fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w,
+                                    done_cnt=done[i, 2] if i + 1 < nl and self.BANK_QKV_WAIT else None)
+                ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=1, ksplit=sd)
+        main.wait_stream(side)
+        return xq, ss_d, tiles, n_ss
+
     def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
         (x' of the next norm -> xq, its sums of squares -> ss_d).  One pg_decode_mlp_block launch at B <= FUSE_MAX_B
@@ -667,6 +752,8 @@ class PaliGemmaEngine:
         merge kernel) whole multiples of 32 such that B * splits stays near DECODE_SPLIT_TARGET -- fewer (O, m, l)
         partials to write and merge once the batch alone fills the chip."""
         SK = self.DECODE_SPLIT_KEYS
+        if self._bank_on(B):
+            return self.BANK_SPLIT_KEYS
         if B <= self.FUSE_MAX_B:
             return self.DECODE_SPLIT_KEYS_SMALL
         blocks = (Smax + SK - 1) // SK

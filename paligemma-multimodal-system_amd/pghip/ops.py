@@ -15,6 +15,7 @@ from . import _lib
 
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN = range(8)
 PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD, PRO_ATTN_INLINE = range(6)
+PRO_X_RSTD_WAIT = 7     # pro 4 whose input comes from another stream (two-stream batch-1 decode)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
 TILE_M1 = 0x400  # OR into epi: all 256..288 rows in one row tile (batch-1 prefill, include/pghip.h PG_TILE_M1)
@@ -223,6 +224,26 @@ def decode_mlp_engine(xq, ss_in, Wgu, Wd, hgran, slab, fin_cnt, resid, ss_out, s
         return False
     if rc != 0:
         raise _lib.PgHipError(f"pg_decode_mlp_engine failed: hip error {rc} ({_lib._err_string(rc)})")
+    return True
+
+
+def gateup_bank(xq, ss_in, Wgu, h, wait_cnt, exit_cnt, err, *, wait_target: int, eps: float = 1e-6) -> bool:
+    """pg_gateup_bank: the batch-1 decode gate/up GEMV (gelu(gate)*up) that loads half of its weights into
+    registers / LDS, then waits for *wait_cnt >= wait_target (an F32_FIN producer on another stream).  Returns
+    False (nothing launched) for shapes it does not cover."""
+    _chk(Wgu, torch.bfloat16, "Wgu")
+    for t, n in ((wait_cnt, "wait_cnt"), (exit_cnt, "exit_cnt"), (err, "err")):
+        _chk(t, torch.int32, n)
+    H = Wgu.shape[1]
+    I = Wgu.shape[0] // 2
+    if h.numel() < I or xq.numel() < H or ss_in.numel() < H // 16:
+        raise ValueError("pghip.gateup_bank: shapes do not match")
+    rc = _lib.load().pg_gateup_bank(_p(xq), _p(ss_in), H // 16, float(eps), _p(Wgu), _p(h), _p(wait_cnt),
+                                    int(wait_target), _p(exit_cnt), _p(err), 1, H, I, _s())
+    if rc == HIP_ERROR_NOT_SUPPORTED:
+        return False
+    if rc != 0:
+        raise _lib.PgHipError(f"pg_gateup_bank failed: hip error {rc} ({_lib._err_string(rc)})")
     return True
 
 

@@ -424,3 +424,63 @@ def test_pt224_mlp_engine_matches_two_launches(golden):
     out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
     eng.MLP_ENGINE = type(eng).MLP_ENGINE
     assert out[0].tolist() == runs[0][0]
+
+
+@pytest.mark.slow
+def test_pt224_two_stream_decode_bit_exact(golden):
+    """The two-stream batch-1 decode layers (_decode_layers_bank: pg_gateup_bank + down on a side stream, the
+    q|k|v GEMV waiting in-kernel for the down projection's done counter) against the one-stream five launches with
+    the same 64-key attention splits: 12 full-size decode steps from the same prefill give bit-identical logits,
+    greedy ids and KV cache, no timed-out wait and every counter re-armed to zero; then the graph-replayed
+    two-stream step (a captured graph with two parallel branches) reproduces the same ids."""
+    from pghip import configs, engine, synthetic, weights
+    g = golden("pt224")
+    cfg = configs.PT_224
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+    ids = torch.from_numpy(g["input_ids"]).cuda()
+    px = torch.from_numpy(g["pixel_values"]).cuda()
+    runs = []
+    for on in (True, False):
+        eng.DECODE_BANK, eng.DECODE_SPLIT_KEYS_SMALL = on, eng.BANK_SPLIT_KEYS
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
+        st = eng.decode_state(1, cache, nxt, 16)
+        eng.sample(logits, st, dict(do_sample=False), advance=False)
+        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
+        torch.cuda.synchronize()
+        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
+    assert eng._bank_ok
+    assert runs[0][0] == runs[1][0]
+    assert torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
+    assert int(eng._ws["d_bank_err"].abs().sum()) == 0
+    assert int(eng._ws["d_bank_cnt"].abs().sum()) == 0
+    assert int(eng._ws["d_fin_cnt"].abs().sum()) == 0
+    eng.DECODE_BANK = True
+    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
+    assert int(eng._ws["d_bank_err"].abs().sum()) == 0
+    eng.DECODE_BANK, eng.DECODE_SPLIT_KEYS_SMALL = type(eng).DECODE_BANK, type(eng).DECODE_SPLIT_KEYS_SMALL
+    assert out[0].tolist() == runs[0][0]
+    assert int(g["greedy_ids"][0]) == runs[0][0][0]
+
+
+def test_gateup_bank_matches_gemv():
+    """pg_gateup_bank alone (its wait already satisfied) against pg_gemm_fused(gate/up, pro 4): the same h bits
+    for random fragment-packed Gemma-2B gate/up weights, x' and per-tile sums of squares; the counters re-arm."""
+    from pghip import ops, weights
+    torch.manual_seed(7)
+    H, I = 2048, 16384
+    w = (torch.randn(2 * I, H, device="cuda") * 0.02).to(torch.bfloat16)
+    wf = weights.frag_pack(w)
+    xq = torch.randn(1, H, device="cuda").to(torch.bfloat16)
+    ss = torch.rand(1, H // 16, device="cuda") * 10
+    h0 = torch.empty(1, I, dtype=torch.bfloat16, device="cuda")
+    fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=H // 16, ss_n=H // 16, eps=1e-6)
+    ops.gemm_fused(xq, wf, h0, fa, epi=ops.EPI_BF16_GELU_MUL | ops.W_FRAG, M=1)
+    cnt = torch.tensor([H // 16], dtype=torch.int32, device="cuda")
+    ex = torch.zeros(1, dtype=torch.int32, device="cuda")
+    er = torch.zeros(1, dtype=torch.int32, device="cuda")
+    h1 = torch.empty_like(h0)
+    assert ops.gateup_bank(xq, ss, wf, h1, cnt, ex, er, wait_target=H // 16)
+    torch.cuda.synchronize()
+    assert int(er) == 0 and int(cnt) == 0 and int(ex) == 0
+    assert torch.equal(h0, h1)

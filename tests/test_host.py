@@ -55,7 +55,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == 2
+    assert lib.pg_abi_version() == 3
 
 
 def test_no_cpu_fallback():
