@@ -759,6 +759,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_XLDS
 #define PG_GEMV_XLDS 0
 #endif
+#ifndef PG_GEMV_HOT
+#define PG_GEMV_HOT 1           // 1 = q|k|v, 2 = o_proj (merge prologue), 3 = both read their weights with
+                                // default-policy loads (allocating in the Infinity Cache) while the others stay nt:
+                                // the 18 layers' q|k|v (189 MB) then stay on-die across decode steps; pt-224 B=1
+                                // A/B/A/B 1.1348/1.1363 -> 1.1325/1.1314 ms/token (2: neutral; 3: 1.142, they no
+                                // longer fit; scripts/r02/gpu_s3f.sh)
+#endif
 #ifndef PG_GEMV_FRAG_NT
 #define PG_GEMV_FRAG_NT 1
 #endif
@@ -1156,11 +1163,11 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 #pragma unroll
         for (int s = 0; s < U; ++s) {
           const u32x4* src = (const u32x4*)(wfrag[t] + ((size_t)cc * U + s) * 512 + lane * 8);
-#if PG_GEMV_FRAG_NT
-          wv[t][s] = __builtin_nontemporal_load(src);
-#else
-          wv[t][s] = *src;
-#endif
+          constexpr bool hot = ((PG_GEMV_HOT & 1) && EPI == PG_EPI_QKV_ROPE) || ((PG_GEMV_HOT & 2) && PRO == 2);
+          if constexpr (PG_GEMV_FRAG_NT && !hot)
+            wv[t][s] = __builtin_nontemporal_load(src);
+          else
+            wv[t][s] = *src;
         }
     } else {
       const int off = (c0 + wave + j * 4) * CH + LANE_OFF;
