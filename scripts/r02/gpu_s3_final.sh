@@ -19,6 +19,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/dprof -o run --output-f
 python scripts/step_timeline.py $O/dprof/run_kernel_trace.csv > $O/decode_step_timeline.txt
 cat $O/decode_step_timeline.txt
 timeout -k 10 400 python bench.py --batch 16 --no-cpu-baseline > $O/bench_pt224_b16.json 2> $O/bench_pt224_b16.err || { tail -5 $O/bench_pt224_b16.err; exit 1; }
+timeout -k 10 400 python bench.py --batch 64 --no-cpu-baseline --steps 2 --warmup 1 > $O/bench_pt224_b64.json 2> $O/bench_pt224_b64.err || { tail -5 $O/bench_pt224_b64.err; exit 1; }
+echo "224x64 ok"
 timeout -k 10 400 python bench.py --config pt-448 --batch 16 --no-cpu-baseline > $O/bench_pt448_b16.json 2> $O/bench_pt448_b16.err || { tail -5 $O/bench_pt448_b16.err; exit 1; }
 echo "448 ok"
 timeout -k 10 500 python bench.py --config pt-896 --batch 32 --fp8 --no-cpu-baseline --steps 3 --warmup 1 > $O/bench_pt896_b32_fp8.json 2> $O/bench_pt896_b32_fp8.err || { tail -5 $O/bench_pt896_b32_fp8.err; exit 1; }
