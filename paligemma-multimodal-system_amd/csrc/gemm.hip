@@ -1629,7 +1629,10 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   // PG_GEMV_D_NT2 / PG_GEMV_D_NT1 (environment, tuning A/B only): ring depth of the two-tile / one-tile kernels
   static const int d2 = getenv("PG_GEMV_D_NT2") ? atoi(getenv("PG_GEMV_D_NT2")) : PG_GEMV_D2;
   static const int d1 = getenv("PG_GEMV_D_NT1") ? atoi(getenv("PG_GEMV_D_NT1")) : 8;
-  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
+  // PG_FIN_NT2 (environment, tuning A/B; the engine reads the same switch for the sums-of-squares layout): the
+  // batch-1 down projection (F32_FIN, split K) as tile pairs too -- half the workgroups, each streaming 2 tiles
+  static const bool fin_nt2 = getenv("PG_FIN_NT2") && atoi(getenv("PG_FIN_NT2")) != 0;
+  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4 || (EPI == PG_EPI_F32_FIN && PRO == 0 && ksplit > 1 && fin_nt2)) {
     const dim3 grid((ntiles + 1) / 2, ksplit);
     if (d2 == 2) launch_gemv_cpw<EPI, 2, 2, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
     else if (d2 == 3) launch_gemv_cpw<EPI, 2, 3, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);

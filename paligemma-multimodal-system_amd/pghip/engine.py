@@ -106,6 +106,9 @@ class PaliGemmaEngine:
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
+    # tuning A/B (read by the library too): the batch-1 down projection as tile pairs, so its per-tile sums of
+    # squares come one per pair
+    FIN_NT2 = os.environ.get("PG_FIN_NT2", "0") not in ("", "0")
     # B = 1, single rank: two-stream decode layers (_decode_layers_bank) -- the gate/up GEMV (pg_gateup_bank) and
     # the down projection run on a side stream, each gate/up launched when the previous down ends so it loads half
     # its weights on-chip while the q|k|v -> attention -> o_proj chain runs; the q|k|v GEMV likewise issues its
@@ -573,6 +576,7 @@ class PaliGemmaEngine:
         so, sd = self._split_o(B), self.split_down
         tiles = (H + 15) // 16
         n_ss = tiles if B <= 4 else (tiles + 1) // 2         # one entry per GEMV workgroup (M > 4: tile pairs)
+        n_ss_d = (tiles + 1) // 2 if self.FIN_NT2 and self.split_down > 1 else n_ss   # the down projection's
         merge_in_gemv = B <= self.FUSE_MAX_B
         attn = None if merge_in_gemv else self._buf("d_attn", (B, nh * hd), torch.bfloat16)
         cnt = self._zeros("d_fin_cnt", (tiles,), torch.int32)
@@ -600,7 +604,7 @@ class PaliGemmaEngine:
                     fq = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                         **rope)
                 else:
-                    fq = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
+                    fq = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
                 fo = ops.fused_args(part_o=part_o, part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt,
                                     q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt,
                                     fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
@@ -620,7 +624,7 @@ class PaliGemmaEngine:
                                     **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             fused = self.FUSE_ATTN_O and nsplit <= 16 and merge_in_gemv
             if not fused:
@@ -649,7 +653,7 @@ class PaliGemmaEngine:
                 ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
             self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
-        return xq, ss_d, tiles, n_ss
+        return xq, ss_d, tiles, n_ss_d
 
     def _bank_on(self, B: int) -> bool:
         w = self.w
@@ -672,6 +676,7 @@ class PaliGemmaEngine:
         kvd = nkv * hd
         so, sd = self._split_o(1), self.split_down
         nl = len(w.tl)
+        n_ss_d = (tiles + 1) // 2 if self.FIN_NT2 and sd > 1 else n_ss
         # per layer: [0] o_proj tiles done, [1] gate/up workgroups past the wait, [2] down tiles done, [3] q|k|v
         # workgroups past the wait -- each on a 256-byte line of its own
         done = self._zeros("d_bank_cnt", (nl, 4, 64), torch.int32)
@@ -689,13 +694,13 @@ class PaliGemmaEngine:
                                     **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
             elif self.BANK_QKV_WAIT:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD_WAIT, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6,
-                                    wait_cnt=done[i - 1, 2], wait_target=tiles, exit_cnt=done[i - 1, 3], err=err,
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD_WAIT, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6,
+                                    wait_cnt=done[i - 1, 2], wait_target=n_ss_d, exit_cnt=done[i - 1, 3], err=err,
                                     **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
             else:
                 main.wait_stream(side)
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
@@ -715,7 +720,7 @@ class PaliGemmaEngine:
                                     done_cnt=done[i, 2] if i + 1 < nl and self.BANK_QKV_WAIT else None)
                 ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=1, ksplit=sd)
         main.wait_stream(side)
-        return xq, ss_d, tiles, n_ss
+        return xq, ss_d, tiles, n_ss_d
 
     def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
