@@ -477,8 +477,9 @@ extern "C" int pg_argmax_embed(const float* logits, long ld, int B, int V, void*
   int* pi = (int*)(pv + B * AM_CHUNKS);
   const AmEmbArgs ea{(const bf16_t*)embed, V_embed, n_feat, H, feat, (int64_t)image_id, (int64_t)pad_id,
                      img_scale, normalizer, res};
-  // PG_ARGMAX_ONEPASS=0 (environment, tuning A/B): the partial and final passes as two launches
-  static const bool onepass = !(getenv("PG_ARGMAX_ONEPASS") && atoi(getenv("PG_ARGMAX_ONEPASS")) == 0);
+  // PG_ARGMAX_ONEPASS=1 (environment, tuning A/B): one launch, the ticketed last workgroup finishing -- neutral at
+  // batch 1, slower at batch 16 (its 4 waves run the final pass and the embedding of every row), so off
+  static const bool onepass = getenv("PG_ARGMAX_ONEPASS") && atoi(getenv("PG_ARGMAX_ONEPASS")) != 0;
   if (onepass) {
     hipLaunchKernelGGL(argmax_embed_onepass_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi, B,
                        out_ids, hist, hist_rows, step, pos, kv_len, ea);

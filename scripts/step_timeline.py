@@ -6,7 +6,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("embed_merge") and int(r["Grid_Size_X"]) <= 16384]
 if len(idx) < 3:    # chained greedy decode (no embed launch): steps end at the argmax's final launch
-    idx = [i + 1 for i, r in enumerate(rows) if r["Kernel_Name"].startswith("argmax_final")]
+    idx = [i + 1 for i, r in enumerate(rows) if r["Kernel_Name"].startswith(("argmax_final", "argmax_embed_onepass"))]
 segs = [(int(rows[b]["Start_Timestamp"]) - int(rows[a]["Start_Timestamp"]), a, b) for a, b in zip(idx, idx[1:])]
 segs = sorted(s for s in segs if s[2] - s[1] < 400)   # decode steps only (prefill spans hundreds of kernels)
 _, i0, i1 = segs[len(segs) // 2]
