@@ -90,12 +90,26 @@ def time_dominant_kernel(eng, reps=50):
     h = torch.empty(1, w.inter, dtype=torch.bfloat16, device="cuda")
     for _ in range(5):
         ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
-    # rotate over the 18 layers' weights so every launch streams from HBM (no L2/MALL reuse)
+    # rotate over the 18 layers' weights so every launch streams from HBM (no L2/MALL reuse).  The launches are
+    # replayed from a captured graph: issued eagerly, a slow host (~40 us per Python launch on some boxes) cannot
+    # keep ahead of 21 us kernels, and the events would time the host instead of the kernel
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g):
+        for i in range(reps):
+            ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
+    g.replay()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    for _ in range(4):          # keep the stream busy while the host enqueues the timed replay
+        ops.gemm(x, L0["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
     ev0.record()
-    for i in range(reps):
-        ops.gemm(x, w.tl[i % len(w.tl)]["gu_w"], h, epi=ops.EPI_BF16_GELU_MUL | w.wflag)
+    g.replay()
     ev1.record()
     torch.cuda.synchronize()
     avg_s = ev0.elapsed_time(ev1) / 1e3 / reps
