@@ -227,26 +227,52 @@ def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
     out = {"tp": world, "comm": "pg_allreduce_xgmi (decode) + RCCL (beyond its buffer)", "scaling": "strong",
            "workload": "the same request (batch 1) split over all GPUs"}
     comm = None
-    try:
+    state = {}
+
+    def phase(name, fn):
+        # every rank runs the phase, then all agree on its outcome (MIN of an ok flag): a failure on one rank makes
+        # every rank stop here together, so no rank is left waiting in a later collective of a phase the others skipped
+        err = None
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 (reported in the JSON line)
+            err = f"{name}: {type(e).__name__}: {e}"
+        ok = torch.tensor([0 if err else 1], device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if err:
+            out["error"] = err[:300]
+        elif not int(ok.item()):
+            out["error"] = f"{name}: failed on another rank"
+        return int(ok.item()) == 1
+
+    def make_comm():
+        nonlocal comm
         comm = XgmiComm()
-        # sanity exchange before any timed work: rank-dependent values summed exactly, no timeout, on every rank
+
+    def sanity():
+        # rank-dependent values summed exactly, no timeout, on every rank
         t = torch.full((4096,), float(rank + 1), device="cuda")
         comm.all_reduce(t)
         torch.cuda.synchronize()
-        ok = int(comm.err.item()) == 0 and bool((t == world * (world + 1) / 2).all())
-        okt = torch.tensor([1 if ok else 0], device="cuda")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        if not int(okt.item()):
-            raise RuntimeError("xGMI sanity all-reduce failed on some rank")
+        if not (int(comm.err.item()) == 0 and bool((t == world * (world + 1) / 2).all())):
+            raise RuntimeError("xGMI sanity all-reduce gave a wrong sum or timed out")
+
+    def build():
         eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
                                      comm=comm)
-        run = Runner(eng, ids[:1], px[:1], T, dict(do_sample=False), False, rank)
+        state["eng"] = eng
+        state["run"] = Runner(eng, ids[:1], px[:1], T, dict(do_sample=False), False, rank)
+        state["run"].request()
+        torch.cuda.synchronize()
+        comm.check()
 
-        def barrier():
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-        run.request()
+    def barrier():
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed():
+        run = state["run"]
         barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -269,9 +295,11 @@ def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
         comm.check()
         out.update(tokens_per_s=round(T * steps / el.item(), 2), ms_per_request=round(el.item() / steps * 1e3, 3),
                    prefill_ms=round(pf_ms, 3), decode_ms_per_token=round(dec, 4), decode=run.graph_mode)
-        del run, eng
-    except Exception as e:  # reported in the JSON line, the data-parallel measurement stands
-        out["error"] = f"{type(e).__name__}: {e}"[:300]
+
+    for name, fn in (("xgmi setup", make_comm), ("xgmi sanity", sanity), ("tp engine", build), ("tp timing", timed)):
+        if not phase(name, fn):
+            break
+    state.clear()
     if comm is not None:
         try:
             comm.close()
