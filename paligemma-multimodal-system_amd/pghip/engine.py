@@ -64,8 +64,10 @@ class KVStore:
 
 class PaliGemmaEngine:
     DECODE_SPLIT_O = 2      # split-K of o_proj at decode (B > FUSE_MAX_B: more workgroups for the batched GEMV)
-    DECODE_SPLIT_O_SMALL = 1  # ... at B <= FUSE_MAX_B: unsplit, the GEMV finalises its own tile (no slab, no ticket;
-                              # 1.120-1.122 vs 1.123-1.127 ms/token at split 2)
+    DECODE_SPLIT_O_SMALL = 2  # ... at B <= FUSE_MAX_B: split 2 (256 workgroups, tile finalised by the second arriver).
+                              # Unsplit won earlier this round (1.120-1.122 vs 1.123-1.127 ms/token); with the q|k|v
+                              # weights Infinity-Cache resident split 2 wins 7 of 8 interleaved pairs, -3.7 us mean
+                              # (scripts/r02/gpu_s3r.sh)
     DECODE_SPLIT_DOWN = 8   # split-K of down_proj at decode (8 vs 4: -4..6 us per pt-224 step, scripts/r02/gpu_t.sh)
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # keys per split at B <= FUSE_MAX_B: every o_proj workgroup merges all active splits in its prologue, so

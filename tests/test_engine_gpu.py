@@ -340,7 +340,7 @@ def test_pt224_fused_decode_block_bit_exact(golden):
     px = torch.from_numpy(g["pixel_values"]).cuda()
     runs = []
     for fused in (True, False):
-        eng.FUSE_BLOCK, eng.split_o = fused, 1
+        eng.FUSE_BLOCK, eng.split_o, eng.DECODE_SPLIT_O_SMALL = fused, 1, 1
         cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
         st = eng.decode_state(1, cache, nxt, 16)
         eng.sample(logits, st, dict(do_sample=False), advance=False)
@@ -354,6 +354,7 @@ def test_pt224_fused_decode_block_bit_exact(golden):
     assert int(sync[3]) == 0 and int(sync[:3].abs().sum()) == 0
     eng.FUSE_BLOCK, eng.split_o = type(eng).FUSE_BLOCK, type(eng).DECODE_SPLIT_O
     out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
+    eng.DECODE_SPLIT_O_SMALL = type(eng).DECODE_SPLIT_O_SMALL
     assert out[0].tolist() == runs[0][0]
     assert int(g["greedy_ids"][0]) == runs[0][0][0]
 
