@@ -21,7 +21,11 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 3: PgFusedArgs two-stream fields, pg_gateup_bank */
+int pg_abi_version(void);   /* 4: the measured-slower decode variants and their PgFusedArgs fields removed */
+/* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
+ * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
+ * Returns hipErrorInvalidValue (truncated) when n < 65. */
+int pg_source_hash(char* out, int n);
 
 /* Epilogues of pg_gemm */
 enum {
@@ -43,7 +47,6 @@ enum {
 typedef struct PgFusedArgs {
   int pro_mode;             /* 0: x = A ; 1: x = RMSNorm(resid_in + sum partials)*(1+norm_w) (gemma.py:172-181) ;
                                2: x = merge of split-KV attention partials (pg_attn_combine folded in) ;
-                               5: as 2, the attention itself computed in the same launch (pg_attn_oproj only) ;
                                3: x = resid_in*(1+norm_w), rstd from ss_in applied to the outputs (RMSNorm of a
                                   residual finalised by a PG_EPI_F32_FIN producer) ;
                                4: x = A (the producer's fin_x = bf16(resid*(1+norm_w))), rstd from ss_in applied
@@ -80,16 +83,6 @@ typedef struct PgFusedArgs {
   int slab_rows;            /* PG_EPI_F32 split-K: rows between slabs (slab z of row m at C + (z*slab_rows + m)*ldc);
                                0 = M.  Lets a GEMM be issued as row blocks that write into one [ksplit][rows][N]
                                partial tensor (C pointing at the block's first row)                            */
-  /* two-stream batch-1 decode (pghip engine; the producer and the consumer run on different streams):
-   * done_cnt   PG_EPI_F32_FIN: residual, x' and sums of squares stored write-through, then +1 per finalised tile;
-   * wait_cnt   pro_mode 7 (= pro 4, batch-1 q|k|v): weights issued first, then wait until *wait_cnt >= wait_target,
-   *            x' and ss_in read with agent-scope loads; exit_cnt: the grid's last workgroup past the wait re-arms
-   *            *wait_cnt and *exit_cnt to 0; err: set to 1 if the wait gave up (0.2 s)                        */
-  int* done_cnt;
-  const int* wait_cnt;
-  int wait_target;
-  int* exit_cnt;
-  int* err;
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -117,17 +110,6 @@ int pg_gemm(const void* A, int lda, const void* W, int ldw, const float* bias, v
             int M, int N, int K, int epi, int ksplit, const float* aux, int aux_rows, void* aux_out,
             int aux_ld, int aux_n, hipStream_t stream);
 
-/* Decode attention + o_proj in one launch (batch <= 2): the split-KV attention of pg_attention's decode mode
- * (gemma.py:307-339, keys in split_keys blocks, fused->asplit <= 16 splits) is computed by the first
- * ceil(B*Hkv*asplit/4) workgroups of the o_proj GEMV (gemma.py:356) while the others stream their weights;
- * every workgroup then merges the partials of its K range and multiplies (fused->pro_mode must be 5; the other
- * fused fields as for pro_mode 2, plus the PG_EPI_F32_FIN fields).  sync: int[3], zero before the first call,
- * self-resetting; sync[2] becomes 1 if a wait gave up (bounded spin). */
-int pg_attn_oproj(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const void* vt,
-                  long vt_bs, long vt_hs, long vt_ds, int B, const int* lkv_dev, int Hq, int Hkv, int D, float scale,
-                  int split_keys, int* sync, const void* W, int ldw, void* C, int ldc, int N, int K, int epi,
-                  int ksplit, const PgFusedArgs* fused, hipStream_t stream);
-
 /* Split-K finalisation: C = epilogue(sum_z part[z]) for a GEMM first run with PG_EPI_F32 into nsplit fp32 slabs
  * [z][M][N] (bias in slab 0).  epi: PG_EPI_BF16 / _GELU / _GELU_MUL / _VT (aux_out, aux_ld, aux_n) / _QKV_ROPE
  * (fused).  Lets a small-M prefill GEMM with a non-linear epilogue split K across CUs. */
@@ -143,69 +125,6 @@ int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* b
 int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                      const float* b, void* out, int ldo, float* out_f32, const int* row_map, int M_out,
                      int H, int mode, float eps, int write_resid, hipStream_t stream);
-
-/* Decode attention block in ONE launch (batch <= 2, head_dim 256, single rank): the q|k|v GEMV (fq: pro 1 or 4,
- * RoPE + KV append) -> split-KV attention (waves of the same launch; q and the new k / v rows handed over
- * write-through through pub_k / pub_v [M][Hkv*256] bf16) -> merge + o_proj GEMV + split-K finalisation (fo:
- * the PG_EPI_F32_FIN and merge fields; akeys = 32, asplit <= 16).  Replaces pg_gemm_fused(q|k|v) + pg_attention
- * + pg_gemm_fused(o_proj) of a decode layer: gemma.py:264-358 + KVCache.update :18-57.  sync: 4 zeroed ints
- * (self-resetting; sync[3] = 1 if a wait timed out).  Returns hipErrorNotSupported with nothing launched when
- * the grid cannot be co-resident on this device (the caller then runs the three launches). */
-int pg_decode_attn_block(const void* xq, const void* wqkv, void* qbuf, const PgFusedArgs* fq, const void* wo,
-                         float* oslab, const PgFusedArgs* fo, int ksplit_o, int M, int H, void* pub_k, void* pub_v,
-                         int* sync, hipStream_t stream);
-
-/* Diagnostics: every later pg_decode_attn_block launch records per workgroup [start, end of its wait, end, -]
- * (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
-int pg_decode_block_stamps(void* buf);
-
-/* Decode MLP block in ONE launch (batch <= 2, single rank, fragment-packed weights): the gate/up GEMV (x' = xq
- * [M][H] from a PG_EPI_F32_FIN producer, rstd from its per-tile sums ss_in; gelu(gate)*up -> h [M][I] bf16) and the
- * down GEMV split `ksplit` ways over K (write-through partials slab [ksplit][M][H] fp32, then the last-arriving split
- * of each 16-column tile adds them into resid in split order, writes ss_out [M][ss_ld_out] and, with norm_w,
- * fin_x = bf16(resid*(1+norm_w))).  Replaces GemmaMLP.forward (gemma.py:210-218) + the residual add (:413-418)
- * of a decode step, i.e. pg_gemm_fused(gate/up, pro 4) + pg_gemm_fused(down, PG_EPI_F32_FIN, ksplit), with
- * identical outputs.  Requires I/16 == (H/16)*ksplit (one workgroup per gate/up tile pair and per down unit).
- * fin_cnt: H/16 zeroed tickets (self-resetting); sync: 640 zeroed ints (self-resetting; sync[576] = 1 if a wait
- * timed out).  Returns hipErrorNotSupported with nothing launched when the grid cannot be co-resident. */
-int pg_decode_mlp_block(const void* xq, const float* ss_in, int ss_ld, int ss_n, float eps, const void* wgu,
-                        void* h, const void* wd, float* slab, int ksplit, int* fin_cnt, float* resid,
-                        float* ss_out, int ss_ld_out, void* fin_x, const float* norm_w, int* sync, int M, int H,
-                        int I, hipStream_t stream);
-
-/* Decode MLP engine (batch 1, Gemma-2B shapes, single rank): the same computation as pg_decode_mlp_block as one
- * persistent launch of 256 two-wave workgroups (one per CU): a loader wave streams the CU's gate/up and down weight
- * slices into a ring of LDS slots by LDS-DMA (running ahead of every dependency), a consumer wave multiplies out of
- * LDS; h is handed over as 8-byte {bf16 pair, epoch tag} granules (hgran: I/2 u64, any initial content), the down
- * projection is split in two k-halves (slab: 2*H fp32) and the second-arriving half finalises the tile into resid,
- * ss_out (H/16) and fin_x.  fin_cnt: H/16 zeroed ints; sync: 192 zeroed ints (self-managing; sync[128] = 1 if a
- * wait timed out).  Replaces gemma.py:210-218 + :413-418 of a decode step.  Returns hipErrorNotSupported with
- * nothing launched for other shapes or when one workgroup per CU cannot cover the 256-workgroup grid. */
-int pg_decode_mlp_engine(const void* xq, const float* ss_in, int ss_n, float eps, const void* wgu, const void* wd,
-                         void* hgran, float* slab, int* fin_cnt, float* resid, float* ss_out, void* fin_x,
-                         const float* norm_w, int* sync, int M, int H, int I, hipStream_t stream);
-/* Diagnostics: every later pg_decode_mlp_engine launch records per CU [start, h published, h half gathered,
- * down done, end, -, -, -] (100 MHz wall clock, u64) into buf [256][8]; null turns it off. */
-int pg_decode_mlp_engine_stamps(void* buf);
-
-/* Batch-1 decode gate/up GEMV that banks half its weights on-chip before its input exists (csrc/decode_bank.hip):
- * launched on a second stream beside the q|k|v -> attention -> o_proj chain, one workgroup per CU loads tile pair
- * 0 of its four into registers and pair 1 into LDS, waits until *wait_cnt >= wait_target (the o_proj F32_FIN
- * producer's done_cnt), then computes h = gelu(rstd*gate)*(rstd*up) bit-identically to
- * pg_gemm_fused(gate/up, PG_EPI_BF16_GELU_MUL | PG_W_FRAG, pro_mode 4) while pairs 2 and 3 stream.  Replaces
- * GemmaMLP gate_proj/up_proj + gelu*up (modeling_gemma.py:210-218) at batch 1.  wait_cnt / exit_cnt: zeroed
- * once, self re-arming.  hipErrorNotSupported unless M == 1, H == 2048, I == 16384. */
-int pg_gateup_bank(const void* xq, const float* ss_in, int ss_n, float eps, const void* wgu, void* h,
-                   const int* wait_cnt, int wait_target, int* exit_cnt, int* err, int M, int H, int I,
-                   hipStream_t stream);
-int pg_gateup_bank_stamps(void* buf);
-/* Diagnostics: every later GEMV launch (M <= 16) k records its workgroups' start / end wall clock (100 MHz) into
- * slot k % 128 of buf [128][2048][2] u64; null turns it off. */
-int pg_gemv_stamps(void* buf);
-
-/* Diagnostics: every later pg_decode_mlp_block launch records per workgroup [start, h published, h slice ready,
- * end] (100 MHz wall clock, u64) into buf [grid][4]; null turns it off. */
-int pg_decode_mlp_stamps(void* buf);
 
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
@@ -273,10 +192,6 @@ int pg_image_preprocess(const uint8_t* src, int H, int W, int S, const int* hb, 
 /* name-seeded synthetic weights, bit-identical to oracle/synth.py (out_kind 0 bf16, 1 f32). */
 int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, int out_kind,
                   hipStream_t stream);
-
-/* Read [p, p + bytes) and discard it (weights pulled into the Infinity Cache ahead of the kernel that
- * streams them; no reference counterpart: a scheduling aid of the decode graph).  policy 1 = nt loads. */
-int pg_prefetch(const void* p, long bytes, int wgs, int policy, hipStream_t stream);
 
 /* fp8 row quantisation feeding PG_FP8 GEMMs: q[m][k] = e4m3(x[m][k] / scale[m]), scale[m] = max|x[m][:]| / 448
  * (1 for an all-zero row).  x bf16 (row stride ldx), q bytes (row stride ldq).  K, ldx, ldq multiples of 8. */

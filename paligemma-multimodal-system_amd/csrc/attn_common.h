@@ -1,5 +1,5 @@
-// Attention pieces shared by attn.hip (the attention kernels) and gemm.hip (the decode o_proj GEMV that
-// computes the split-KV attention in-kernel, pg_attn_oproj).
+// Attention pieces of attn.hip (the prefill / decode attention kernels): arguments, guarded loads, and the
+// one-wave split-KV decode block.
 #pragma once
 #include "common.h"
 
@@ -17,28 +17,7 @@ struct AttnArgs {
   float* part_ml;          // [B][Hkv][nsplit][16][2]
   int kcap;                // decode: key rows readable per (b, kv head) in K and V^T (the static cache's Smax);
                            // > 0 lets a split issue its first block's loads before the kv length arrives
-  // FUSED decode (pg_decode_attn_block): q|k|v are produced in the same launch -- wait until *wait_cnt reaches
-  // wait_target, then read q and the new token's k / v rows (pub_k / pub_v [B][Hkv*D]) write-through
-  const int* wait_cnt;
-  int wait_target;
-  const bf16_t* pub_k;
-  const bf16_t* pub_v;
-  int* err;                // set to 1 when the wait gives up (bounded by the wall clock)
-  unsigned long long* stamps;   // diagnostics (pg_decode_block_stamps): [blockIdx.x][4], [1] = end of the wait
 };
-
-#ifndef PG_ATT_TIMEOUT_TICKS
-#define PG_ATT_TIMEOUT_TICKS 20000000ull    // 0.2 s of the 100 MHz constant clock
-#endif
-
-// 16 bytes as two write-through-readable (sc1) 8-B loads of bf16 data
-static __device__ __forceinline__ u32x4 ld16_wt_u(const bf16_t* p) {
-  typedef __attribute__((address_space(1))) unsigned long long gu64_;
-  const gu64_* q = (const gu64_*)p;
-  const u32x2 a = __builtin_bit_cast(u32x2, __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const u32x2 b = __builtin_bit_cast(u32x2, __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  return u32x4{a[0], a[1], b[0], b[1]};
-}
 
 // Branch-free guarded loads: the address is always valid (callers clamp it), the value is
 // zeroed by selects.  Conditional loads compiled to branches and, for partial blocks, to
@@ -86,12 +65,8 @@ static __device__ __forceinline__ f32x2 ld8_wt(const float* p) {
 // stored) -- so hipcc has no reason to wait for a load before the next one is issued, and the kv length is
 // read with a vector load (in order with the stream; a scalar load's lgkmcnt wait lands before the first
 // vector load, behind the kernel-argument loads).
-// FUSED (implies FULL, WT): the q|k|v of this token come from the same launch (AttnArgs wait_cnt / pub_k / pub_v):
-// the cached block is prefetched, then the wave waits, reads q and the new k / v rows write-through and patches
-// the new row into the prefetched registers (its cache line may be stale in this CU's caches).
-template <int DP, int DT, bool WT, bool FULL = false, bool FUSED = false>
+template <int DP, int DT, bool WT, bool FULL = false>
 __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int kvh, int sp, int nsplit, int lane) {
-  static_assert(!FUSED || (FULL && WT), "the fused decode split is a FULL write-through split");
   constexpr int KS = DP / 32;
   const int c = lane & 15, g = lane >> 4;
   const int R = a.Lq * a.G;
@@ -108,15 +83,13 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 
   bf16x8 qf[KS];
   const bf16_t* qp = a.q + ((long)b * a.Lq + pos) * a.q_rs + (long)hq * D;
-  if constexpr (!FUSED) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int d0 = 32 * s + 8 * g;
-      if constexpr (FULL)
-        qf[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qp + d0));
-      else
-        qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
-    }
+  for (int s = 0; s < KS; ++s) {
+    const int d0 = 32 * s + 8 * g;
+    if constexpr (FULL)
+      qf[s] = __builtin_bit_cast(bf16x8, *(const u32x4*)(qp + d0));
+    else
+      qf[s] = __builtin_bit_cast(bf16x8, ld16_sel(qp + (d0 < D ? d0 : 0), rvalid && d0 < D));
   }
   const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
   const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
@@ -157,53 +130,6 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   u32x2 vr[DT][2];
   if (FULL) load_block(min(kbeg, a.kcap - 32), a.kcap, kfa, kfb, vr);
   else if (pre) load_block(kbeg, a.kcap, kfa, kfb, vr);
-  if constexpr (FUSED) {
-    // wait for the q|k|v projection of this token (one lane polls; the wave reconverges after the loop)
-    if (lane == 0) {
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(a.wait_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.wait_target) {
-        if (wall_clock64() - t0 > PG_ATT_TIMEOUT_TICKS) {
-          __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 4 + 1] = wall_clock64();
-    }
-    __builtin_amdgcn_wave_barrier();
-    const bf16_t* kn = a.pub_k + ((long)b * a.Hkv + kvh) * D;
-    const bf16_t* vn = a.pub_v + ((long)b * a.Hkv + kvh) * D;
-    u32x4 knew[KS];
-    uint32_t vnew[DT];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int d0 = 32 * s + 8 * g;
-      qf[s] = __builtin_bit_cast(bf16x8, ld16_wt_u(qp + d0));
-      knew[s] = ld16_wt_u(kn + d0);
-    }
-#pragma unroll
-    for (int t = 0; t < DT; ++t)   // the 32-bit word holding v_new[16t + c]
-      vnew[t] = __hip_atomic_load((const uint32_t*)(vn + ((16 * t + c) & ~1)), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-    // patch the new token's row (key kvpos = the kv length before it) into the prefetched block
-    const int kvpos = __builtin_amdgcn_readfirstlane(lkv_raw);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (kbeg + c == kvpos) kfa[s] = knew[s];
-      if (kbeg + 16 + c == kvpos) kfb[s] = knew[s];
-    }
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint32_t nv = (c & 1) ? (vnew[t] >> 16) : (vnew[t] & 0xFFFFu);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = kvpos - (kbeg + 16 * h + 4 * g);     // element of this lane's 4-key run
-        const uint32_t w0 = vr[t][h][0], w1 = vr[t][h][1];
-        vr[t][h][0] = j == 0 ? ((w0 & 0xFFFF0000u) | nv) : (j == 1 ? ((w0 & 0xFFFFu) | (nv << 16)) : w0);
-        vr[t][h][1] = j == 2 ? ((w1 & 0xFFFF0000u) | nv) : (j == 3 ? ((w1 & 0xFFFFu) | (nv << 16)) : w1);
-      }
-    }
-  }
   const int Lkv = (FULL ? __builtin_amdgcn_readfirstlane(lkv_raw) : (a.lkv_dev ? *a.lkv_dev : 0)) + a.Lkv;
   const int kend = min(Lkv, kbeg + a.split_keys);
   // one 32-key block from the loaded registers: mask by the kv length, S^T, online softmax, P.V.  A block with

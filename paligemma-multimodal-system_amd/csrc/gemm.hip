@@ -85,15 +85,6 @@ struct PgFusedArgs {
   const float* a_scale;      // [M]
   const float* w_scale;      // [N] (in W's row order, e.g. the packed q|k|v or interleaved gate/up rows)
   int slab_rows;             // PG_EPI_F32 split-K: rows between slabs (0 = M); lets a GEMM run as row blocks
-  // two-stream decode (pghip engine, batch 1): a PG_EPI_F32_FIN producer stores its finalised residual / x' / sums
-  // of squares write-through and adds 1 per finalised tile to done_cnt; a pro_mode 7 consumer (pro 4 whose input
-  // comes from a launch on ANOTHER stream) issues its weights, waits until *wait_cnt >= wait_target, then reads x'
-  // and ss_in with agent-scope loads; the workgroup whose exit_cnt add is the grid's last re-arms both counters
-  int* done_cnt;
-  const int* wait_cnt;
-  int wait_target;
-  int* exit_cnt;
-  int* err;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -120,19 +111,6 @@ struct EpiArgs {
   int aux_ld;
   int aux_n;
   PgFusedArgs f;
-  // pro_mode 5 (pg_attn_oproj): the first att_wgs workgroups compute the split-KV decode attention (4 splits
-  // each, write-through partials), then every workgroup waits on sync[0] and merges; sync[1] counts the
-  // workgroups done, the last resets both; sync[2] = 1 if a wait gave up
-  AttnArgs att;
-  int att_total;             // B * Hkv * nsplit splits
-  int att_wgs;
-  int* sync;
-  // decode attention block (pg_decode_attn_block): the q|k|v epilogue publishes for consumers in the same launch --
-  // q stored write-through, the new k / v rows also write-through to pub_k / pub_v [B][Hkv*D]
-  int pub;
-  bf16_t* pub_k;
-  bf16_t* pub_v;
-  unsigned long long* stamps;   // diagnostics (pg_decode_block_stamps): [blockIdx.x][4], [1] = end of the PRO 6 wait
 };
 
 // fp8 dequantisation of one accumulator fragment: C[m][n0..n0+3] *= a_scale[m] * w_scale[n0..n0+3]
@@ -177,28 +155,16 @@ __device__ __forceinline__ void epi_qkv_rope4_core(const EpiArgs& e, int m, int 
     u32x2 pk;
     pk[0] = pack_bf2(y[0], y[1]);
     pk[1] = pack_bf2(y[2], y[3]);
-    typedef __attribute__((address_space(1))) unsigned long long gu64;
     if (blk < Hq) {
-      bf16_t* qp = (bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0;
-      if (e.pub) __hip_atomic_store((gu64*)qp, __builtin_bit_cast(unsigned long long, pk), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-      else *(u32x2*)qp = pk;
-    } else {
-      if (in_cache) *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
-      if (e.pub) __hip_atomic_store((gu64*)(e.pub_k + (size_t)b * KV + (blk - Hq) * D + d0),
-                                    __builtin_bit_cast(unsigned long long, pk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0) = pk;
+    } else if (in_cache) {
+      *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
     }
   } else {
     const int c0 = (blk - Hq - Hkv) * D + d0;
     if (in_cache) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
-    }
-    if (e.pub) {
-      typedef __attribute__((address_space(1))) unsigned long long gu64;
-      const u32x2 pv = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
-      __hip_atomic_store((gu64*)(e.pub_v + (size_t)b * KV + c0), __builtin_bit_cast(unsigned long long, pv),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -735,20 +701,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
 #endif
-#ifndef PG_AO_SPLITS_PER_WG
-#define PG_AO_SPLITS_PER_WG 1   // pg_attn_oproj: attention splits per workgroup (one wave each, <= 4)
-#endif
 #ifndef PG_F8_G256
 #define PG_F8_G256 0            // fp8 GEMMs on the 256x256 kernel: it spills at fp8 (2x slower than the 128x128 tile kernel)
 #endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
-#endif
-#ifndef PG_T_NOMERGE
-#define PG_T_NOMERGE 0
-#endif
-#ifndef PG_T_NOFIN
-#define PG_T_NOFIN 0
 #endif
 #ifndef PG_GEMV_QKV_NT1
 #define PG_GEMV_QKV_NT1 1   // batched (M > 4) q|k|v GEMV with one 16-row tile per workgroup
@@ -769,18 +726,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_FRAG_NT
 #define PG_GEMV_FRAG_NT 1
 #endif
-#ifndef PG_BLOCK_TIMEOUT_TICKS
-#define PG_BLOCK_TIMEOUT_TICKS 20000000ull    // 0.2 s of the 100 MHz constant clock: a fused-launch wait gives up
-#endif
 #ifndef PG_GEMV_CPW
 #define PG_GEMV_CPW 1     // decode GEMV: straight-line chunk loop when every wave owns the same chunk count
 #endif
-#ifndef PG_MERGE_V2
-#define PG_MERGE_V2 1
-#endif
 
-// the GEMV's workgroup coordinates: blockIdx / gridDim of its own launch, or a role's virtual ones inside a fused
-// launch (decode_block.hip)
+// the GEMV's workgroup coordinates (blockIdx / gridDim of its launch)
 struct GemvIdx {
   int bx, by, nx, ny;
 };
@@ -884,58 +834,12 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
     }
     __syncthreads();
     if (t < M) red[64 + t] = rsqrtf((red[t] + red[16 + t] + red[32 + t] + red[48 + t]) / (float)K + f.eps);
-  } else if constexpr ((PRO == 2 && PG_MERGE_V2) || PRO == 5 || PRO == 6) {
-    if constexpr (PRO == 6) {
-      // decode attention block (pg_decode_attn_block): the attention waves of the same launch publish their
-      // partials write-through and add to sync[0]; wait for all att_total of them (weights already in flight),
-      // bounded by the wall clock (sync[3] = 1 on a timeout: the outputs are then meaningless)
-      if (t == 0) {
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(e.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.att_total) {
-          if (wall_clock64() - t0 > PG_BLOCK_TIMEOUT_TICKS) {
-            __hip_atomic_store(e.sync + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (e.stamps) e.stamps[blockIdx.x * 4 + 1] = wall_clock64();
-      }
-      __syncthreads();
-    }
-    if constexpr (PRO == 5) {
-      // attention role (workgroups [0, att_wgs)): 4 splits, one per wave; then publish (drained write-through
-      // stores, workgroup barrier, one relaxed agent-scope add).  Every workgroup then waits for all of them.
-      const int wg = gi.by * gi.nx + gi.bx;
-      if (wg < e.att_wgs) {
-        const int id = wg * PG_AO_SPLITS_PER_WG + (t >> 6);
-        if ((t >> 6) < PG_AO_SPLITS_PER_WG && id < e.att_total) {
-          const int ns = f.asplit;
-          const int sp = id % ns, kvh = (id / ns) % e.att.Hkv, b = id / (ns * e.att.Hkv);
-          const int DT = (e.att.D + 15) / 16;
-          if (DT == 16) attn_decode_split<256, 16, true>(e.att, b, kvh, sp, ns, t & 63);
-          else if (DT <= 2) attn_decode_split<32, 2, true>(e.att, b, kvh, sp, ns, t & 63);
-          else if (DT <= 4) attn_decode_split<64, 4, true>(e.att, b, kvh, sp, ns, t & 63);
-          else attn_decode_split<128, 8, true>(e.att, b, kvh, sp, ns, t & 63);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) __hip_atomic_fetch_add(e.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (t == 0) {
-        int n = 0;
-        while (__hip_atomic_load(e.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.att_wgs && ++n < (1 << 20))
-          __builtin_amdgcn_s_sleep(2);
-        if (n >= (1 << 20)) __hip_atomic_store(e.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-    }
-    // one pass per (row, head, 4 dims): online merge over the splits, no LDS staging / barriers
+  } else if constexpr (PRO == 2) {
+    // one pass per (row, head, 4 dims): merge over the splits, no LDS staging / barriers
     const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
     const int h0 = k0 / D, nh = Kr / D, D4 = D >> 2;
-    const int items = PG_T_NOMERGE ? 0 : M * nh * D4;   // PG_T_NOMERGE: timing experiment only (x = 0)
-    if (PG_T_NOMERGE)
-      for (int idx = t; idx < M * Kr / 4; idx += 256) *(u32x2*)(xs + (idx / (Kr / 4)) * ldx + (idx % (Kr / 4)) * 4) = u32x2{0u, 0u};
-    if (S <= 16 && !PG_T_NOMERGE) {
+    const int items = M * nh * D4;
+    if (S <= 16) {
       // every split's (m, l, o) loaded at once (one dependent L2 round trip, no read of the kv length:
       // splits past it hold m = -inf and weigh 0), then a two-pass max / weighted sum
       for (int idx = t; idx < M * nh * D4; idx += 256) {
@@ -950,8 +854,8 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
 #pragma unroll
         for (int sp = 0; sp < 16; ++sp) {
           const long bs = base0 + (long)min(sp, S - 1) * 16;
-          mlv[sp] = PRO >= 5 ? ld8_wt(f.part_ml + bs * 2) : *(const f32x2*)(f.part_ml + bs * 2);
-          o4[sp] = PRO >= 5 ? ld16_wt(f.part_o + bs * f.dtw + d4 * 4) : *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
+          mlv[sp] = *(const f32x2*)(f.part_ml + bs * 2);
+          o4[sp] = *(const f32x4*)(f.part_o + bs * f.dtw + d4 * 4);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -977,15 +881,6 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
       }
       __syncthreads();
-      if ((PRO == 5 || PRO == 6) && t == 0) {
-        const int total = gi.nx * gi.ny;
-        if (__hip_atomic_fetch_add(e.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-          __hip_atomic_store(e.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);       // every wait is over
-          __hip_atomic_store(e.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          // PRO 6: also the q|k|v arrival counter (every attention wave passed its wait before adding to sync[0])
-          if (PRO == 6) __hip_atomic_store(e.sync + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
       return;
     }
     const int Seff = (f.slot_dev && f.akeys > 0) ? min(S, (*f.slot_dev + f.akeys) / f.akeys) : S;
@@ -1012,45 +907,6 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
       pk[0] = pack_bf2(num[0] * inv, num[1] * inv);
       pk[1] = pack_bf2(num[2] * inv, num[3] * inv);
       *(u32x2*)(xs + m * ldx + hl * D + d4 * 4) = pk;
-    }
-  } else if constexpr (PRO == 2) {
-    // x[m][k], k = hq*D + d over this WG's K range; partial row of q head hq: (kvh = hq / G, row = hq % G)
-    const int D = f.head_dim, G = f.q_per_kv, S = f.asplit;
-    const int h0 = k0 / D, nh = Kr / D;
-    float* wsc = scratch;              // [M*nh][S] weights, then [M*nh] 1/den at the end
-    const int pairs = M * nh;
-    for (int idx = t; idx < pairs * S; idx += 256) {
-      const int pr = idx / S, sp = idx % S;
-      const int m = pr / nh, hq = h0 + pr % nh;
-      const long base = (((long)m * f.kv_heads + hq / G) * S + sp) * 16 + (hq % G);
-      wsc[idx] = f.part_ml[base * 2];
-    }
-    __syncthreads();
-    float* inv = scratch + pairs * S;
-    for (int pr = t; pr < pairs; pr += 256) {
-      const int m = pr / nh, hq = h0 + pr % nh;
-      float Mx = -INFINITY;
-      for (int sp = 0; sp < S; ++sp) Mx = fmaxf(Mx, wsc[pr * S + sp]);
-      float den = 0.f;
-      for (int sp = 0; sp < S; ++sp) {
-        const float ms = wsc[pr * S + sp];
-        const float w = ms == -INFINITY ? 0.f : exp2f(ms - Mx);
-        const long base = (((long)m * f.kv_heads + hq / G) * S + sp) * 16 + (hq % G);
-        den += w * f.part_ml[base * 2 + 1];
-        wsc[pr * S + sp] = w;
-      }
-      inv[pr] = 1.0f / den;
-    }
-    __syncthreads();
-    for (int idx = t; idx < M * Kr; idx += 256) {
-      const int m = idx / Kr, kk = idx % Kr;
-      const int hl = kk / D, d = kk % D, hq = h0 + hl;
-      const int pr = m * nh + hl;
-      const long base0 = (((long)m * f.kv_heads + hq / G) * S) * 16 + (hq % G);
-      float num = 0.f;
-#pragma unroll 8
-      for (int sp = 0; sp < S; ++sp) num += wsc[pr * S + sp] * f.part_o[(base0 + (long)sp * 16) * f.dtw + d];
-      xs[m * ldx + kk] = f2bf(num * inv[pr]);
     }
   }
   __syncthreads();
@@ -1097,41 +953,32 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   const int Kr = per_z * CH;                    // K range of this split (LDS row length)
   // rows past M read row M-1 (their outputs are never stored): the x loads are unconditional, so the compiler
   // has no select or branch to resolve and no reason to wait for them before issuing the rest of the stream
-  const bf16_t* xrow = (PRO == 0 || PRO == 4 || PRO == 7) ? A + (size_t)(xvalid ? r : M - 1) * lda : nullptr;
+  const bf16_t* xrow = (PRO == 0 || PRO == 4) ? A + (size_t)(xvalid ? r : M - 1) * lda : nullptr;
   // PRO 4 (M <= 2): wave 0 loads the producer's per-tile sums of squares before the weight stream (all
   // at once, clamped addresses; lanes [32*row, 32*row + 32) own a row) and sums them in the epilogue
   // M > 4 (two tiles per workgroup, <= 64 entries per row): lane (row r, group g) loads entries g + 4k of its
   // own row, so the row total is a reduction over the 4 lane groups
   // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- use the same 16-entry layout as the
   // two-tile form)
-  constexpr bool SS16 = (PRO == 4 || PRO == 7) && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
+  constexpr bool SS16 = PRO == 4 && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
   constexpr int SSL = SS16 ? 16 : 4;
   float ssv[SSL];
 #pragma unroll
   for (int k = 0; k < SSL; ++k) ssv[k] = 0.f;
-  // pro 7: the same entries, read with agent-scope loads after the wait (the producer ran on another stream)
-  auto ldss = [&](const float* p) -> float {
-    if constexpr (PRO == 7)
-      return __uint_as_float(__hip_atomic_load((const __attribute__((address_space(1))) unsigned*)p, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT));
-    else
-      return *p;
-  };
-  auto load_ss = [&]() {
+  if constexpr (PRO == 4) {
     if (wave == 0) {
       if (SS16 && M > 2) {
         const int rr = min(r, M - 1);
 #pragma unroll
-        for (int k = 0; k < SSL; ++k) ssv[k] = ldss(e.f.ss_in + (size_t)rr * e.f.ss_ld + min(g + 4 * k, e.f.ss_n - 1));
+        for (int k = 0; k < SSL; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(g + 4 * k, e.f.ss_n - 1)];
       } else {
         const int lpr = M == 1 ? 64 : 32;
         const int rr = min(lane / lpr, M - 1);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ssv[k] = ldss(e.f.ss_in + (size_t)rr * e.f.ss_ld + min(lane % lpr + k * lpr, e.f.ss_n - 1));
+        for (int k = 0; k < 4; ++k) ssv[k] = e.f.ss_in[(size_t)rr * e.f.ss_ld + min(lane % lpr + k * lpr, e.f.ss_n - 1)];
       }
     }
-  };
-  if constexpr (PRO == 4) load_ss();
+  }
   const bf16_t* xlds = xs + (xvalid ? r : M - 1) * (Kr + XPAD);
   // PG_EPI_QKV_ROPE: the epilogue's rotary positions and cache slot load before the weight stream, its cos/sin
   // right after the first chunks are issued, so the epilogue starts without a dependent round trip
@@ -1185,16 +1032,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   };
   auto loadx = [&](int j, u32x4 (&xv)[U]) {
     const int koff = (wave + j * 4) * CH + LANE_OFF;      // offset inside this split
-    if constexpr (PRO == 7) {
-      typedef __attribute__((address_space(1))) unsigned long long gx64;
-#pragma unroll
-      for (int s = 0; s < U; ++s) {
-        const gx64* px = (const gx64*)(xrow + c0 * CH + koff + S_STRIDE * s);
-        const unsigned long long lo = __hip_atomic_load(px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long hi = __hip_atomic_load(px + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        xv[s] = u32x4{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
-      }
-    } else if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
+    if constexpr ((PRO == 0 || PRO == 4) && !PG_GEMV_XLDS) {
 #pragma unroll
       for (int s = 0; s < U; ++s)
         xv[s] = *(const u32x4*)(xrow + c0 * CH + koff + S_STRIDE * s);
@@ -1203,10 +1041,9 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       for (int s = 0; s < U; ++s) xv[s] = *(const u32x4*)(xlds + koff + S_STRIDE * s);
     }
   };
-  constexpr bool STAGED = (PRO != 0 && PRO != 4 && PRO != 7) || PG_GEMV_XLDS;   // x built in LDS by a prologue
-  // weights issued before the prologue, except by the attention workgroups of pro_mode 5 (their publish
-  // drains vmcnt: the attention result, not their weights, is on everyone's critical path)
-  const bool prew = STAGED && PG_GEMV_PREW && !(PRO == 5 && gi.by * gi.nx + gi.bx < e.att_wgs);
+  constexpr bool STAGED = (PRO != 0 && PRO != 4) || PG_GEMV_XLDS;   // x built in LDS by a prologue
+  // weights issued before the prologue (its loads are the critical path: the stream overlaps them)
+  constexpr bool prew = STAGED && PG_GEMV_PREW;
   if (prew) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
@@ -1220,7 +1057,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   for (int d = 0; d < DEPTH; ++d)
     if (CPW > 0 ? d < CPW : d < mine) {
       if (!prew) loadw(d, wb[d]);
-      if constexpr (PRO != 7) loadx(d, xb[d]);
+      loadx(d, xb[d]);
     }
   // PG_EPI_F32_FIN: the residual rows and norm weights the tile's last-arriving split finalises are loaded now
   // (nothing else writes them in this launch), so the reducer's only round trip is the slab read
@@ -1245,29 +1082,6 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       rope_cs[t] = *(const f32x4*)(e.f.cos_t + off);
       rope_sn[t] = *(const f32x4*)(e.f.sin_t + off);
     }
-  }
-  if constexpr (PRO == 7) {
-    // the weights (and the epilogue's own operands) are in flight: wait for the producer on the other stream
-    if (threadIdx.x == 0) {
-      const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(e.f.wait_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < e.f.wait_target) {
-        if (wall_clock64() - t0 > PG_BLOCK_TIMEOUT_TICKS) {
-          __hip_atomic_store(e.f.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (__hip_atomic_fetch_add(e.f.exit_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-          (int)(gridDim.x * gridDim.y) - 1) {
-        __hip_atomic_store((int*)e.f.wait_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(e.f.exit_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_barrier" ::: "memory");     // (no fence: the weight loads stay in flight)
-    load_ss();
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d)
-      if (CPW > 0 ? d < CPW : d < mine) loadx(d, xb[d]);
   }
   if constexpr (CPW > 0) {
     // sched_barrier: the scheduler may not sink the ring's loads below later MFMAs (it otherwise trades the
@@ -1325,7 +1139,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] *= rs;
   }
-  if constexpr (PRO == 4 || PRO == 7) {
+  if constexpr (PRO == 4) {
     // the raw per-tile entries were loaded with clamped indices (no select before the weight stream): mask here
     float ss = 0.f;
     if (SS16 && M > 2) {
@@ -1356,45 +1170,19 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     // The reducer reads the slabs with sc1 loads (bypass its L1/L2), so no acquire fence either.
     const PgFusedArgs& f = e.f;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
-    // done_cnt (two-stream decode): everything a consumer on the other stream reads is stored write-through
     auto finish = [&](int t, int n0, f32x4 v, float& ssl) {   // v = the finalised residual of (m, n0..n0+3)
-      if (f.done_cnt) {
-        gu64* rp = (gu64*)(f.fin_resid + (size_t)m * e.N + n0);
-        __hip_atomic_store(rp, __builtin_bit_cast(unsigned long long, f32x2{v[0], v[1]}), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(rp + 1, __builtin_bit_cast(unsigned long long, f32x2{v[2], v[3]}), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
-      }
+      *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
       ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
       if (f.fin_x) {
         const f32x4 w = fin_w[t];
         u32x2 pk;
         pk[0] = pack_bf2(v[0] * (1.0f + w[0]), v[1] * (1.0f + w[1]));
         pk[1] = pack_bf2(v[2] * (1.0f + w[2]), v[3] * (1.0f + w[3]));
-        if (f.done_cnt)
-          __hip_atomic_store((gu64*)(f.fin_x + (size_t)m * e.N + n0), __builtin_bit_cast(unsigned long long, pk),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
+        *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
       }
     };
     auto put_ss = [&](float ssl) {
-      if (g == 0 && m < M) {
-        float* sp = f.ss_out + (size_t)m * f.ss_ld + gi.bx;
-        if (f.done_cnt)
-          __hip_atomic_store((__attribute__((address_space(1))) unsigned*)sp, __float_as_uint(ssl), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else
-          *sp = ssl;
-      }
-    };
-    auto arrive = [&]() {   // after this wave's (the only storing wave's) stores have drained
-      if (f.done_cnt) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add(f.done_cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
     };
     if (gi.ny == 1) {
       // no split: this workgroup owns the tile -- no slab, no ticket (same sums: residual + (acc + bias))
@@ -1411,7 +1199,6 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       ssl += __shfl_xor(ssl, 16, 64);
       ssl += __shfl_xor(ssl, 32, 64);
       put_ss(ssl);
-      arrive();
       return;
     }
 #pragma unroll
@@ -1428,7 +1215,6 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (PG_T_NOFIN) return;                                  // timing experiment only: slabs never reduced
     int old = 0;
     if (lane == 0) old = __hip_atomic_fetch_add(f.fin_cnt + gi.bx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     old = __shfl(old, 0, 64);
@@ -1462,7 +1248,6 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     ssl += __shfl_xor(ssl, 32, 64);
     put_ss(ssl);
     if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    arrive();
     return;
   }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
@@ -1487,22 +1272,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 template <int EPI, int NT, int U, int DEPTH, int PRO, bool FRAG, int CPW = 0>
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A, int lda,
                                                    const bf16_t* __restrict__ W, int ldw, int K, EpiArgs e) {
-  // diagnostics (pg_gemv_stamps): start / end of workgroup blockIdx.y * gridDim.x + blockIdx.x (< 2048), thread 0
-  const int sid = blockIdx.y * gridDim.x + blockIdx.x;
-  if (e.stamps && threadIdx.x == 0 && sid < 2048) e.stamps[2 * sid] = wall_clock64();
   gemv_body<EPI, NT, U, DEPTH, PRO, FRAG, CPW>(A, lda, W, ldw, K, e,
                                                GemvIdx{(int)blockIdx.x, (int)blockIdx.y, (int)gridDim.x, (int)gridDim.y});
-  if (e.stamps && threadIdx.x == 0 && sid < 2048) e.stamps[2 * sid + 1] = wall_clock64();
-}
-
-// Diagnostics: with a buffer set, every later GEMV launch (M <= 16) k records its workgroups' start / end wall clock
-// (100 MHz) into slot k % 128 of buf [128][2048][2] u64 (captured launches keep their slot); null turns it off
-static unsigned long long* g_gemv_stamps = nullptr;
-static unsigned g_gemv_launch = 0;
-extern "C" int pg_gemv_stamps(void* buf) {
-  g_gemv_stamps = (unsigned long long*)buf;
-  g_gemv_launch = 0;
-  return 0;
 }
 
 // --------------------------------------------------------------------------------------
@@ -1590,9 +1361,7 @@ static void launch_gemv_cpw(dim3 grid, size_t lds, hipStream_t st, const bf16_t*
                             int K, int ksplit, const EpiArgs& e) {
   const int nch = K / 64;                              // U = 2: 64-element chunks
   const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
-  // PG_GEMV_CPW_OFF=1 (environment, tuning A/B only): the runtime-loop kernel everywhere
-  static const bool cpw_off = getenv("PG_GEMV_CPW_OFF") && atoi(getenv("PG_GEMV_CPW_OFF")) != 0;
-  switch (PG_GEMV_CPW && !cpw_off ? cpw : 0) {
+  switch (PG_GEMV_CPW ? cpw : 0) {
     case 4: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 4>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
     case 8: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 8>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
     case 16: hipLaunchKernelGGL((gemv_kernel<EPI, NT, 2, DEPTH, PRO, FRAG, 16>), grid, dim3(256), lds, st, A, lda, W, ldw, K, e); break;
@@ -1609,15 +1378,11 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   const int CH = 64;                                   // U = 2
   const int per_z = (K / CH + ksplit - 1) / ksplit;
   size_t lds = 0;
-  if ((PRO != 0 && PRO != 4 && PRO != 7) || PG_GEMV_XLDS) {
+  if ((PRO != 0 && PRO != 4) || PG_GEMV_XLDS) {
     lds = (size_t)e.M * (per_z * CH + XPAD) * 2;
     lds = (lds + 15) & ~(size_t)15;
     if (PRO == 1) lds += 64 * sizeof(float);
     if (PRO == 3) lds += 80 * sizeof(float);
-    if (PRO == 2 || PRO == 5) {
-      const int pairs = e.M * (per_z * CH / e.f.head_dim);
-      lds += (size_t)(pairs * e.f.asplit + pairs) * sizeof(float);
-    }
   }
   if constexpr (PG_GEMV_QKV_NT1 && EPI == PG_EPI_QKV_ROPE) {
     if (e.M > 4) {
@@ -1626,22 +1391,11 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
       return;
     }
   }
-  // PG_GEMV_D_NT2 / PG_GEMV_D_NT1 (environment, tuning A/B only): ring depth of the two-tile / one-tile kernels
-  static const int d2 = getenv("PG_GEMV_D_NT2") ? atoi(getenv("PG_GEMV_D_NT2")) : PG_GEMV_D2;
-  static const int d1 = getenv("PG_GEMV_D_NT1") ? atoi(getenv("PG_GEMV_D_NT1")) : 8;
-  // PG_FIN_NT2 (environment, tuning A/B; the engine reads the same switch for the sums-of-squares layout): the
-  // batch-1 down projection (F32_FIN, split K) as tile pairs too -- half the workgroups, each streaming 2 tiles
-  static const bool fin_nt2 = getenv("PG_FIN_NT2") && atoi(getenv("PG_FIN_NT2")) != 0;
-  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4 || (EPI == PG_EPI_F32_FIN && PRO == 0 && ksplit > 1 && fin_nt2)) {
-    const dim3 grid((ntiles + 1) / 2, ksplit);
-    if (d2 == 2) launch_gemv_cpw<EPI, 2, 2, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
-    else if (d2 == 3) launch_gemv_cpw<EPI, 2, 3, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
-    else launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+  // ring depths re-checked on the final round-2 code: two-tile kernels 4 chunks in flight, one-tile 8
+  if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
+    launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(dim3((ntiles + 1) / 2, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   } else {
-    const dim3 grid(ntiles, ksplit);
-    if (d1 == 4) launch_gemv_cpw<EPI, 1, 4, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
-    else if (d1 == 6) launch_gemv_cpw<EPI, 1, 6, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
-    else launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(grid, lds, st, A, lda, W, ldw, K, ksplit, e);
+    launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   }
 }
 
@@ -1653,12 +1407,6 @@ static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
     case 2: launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 3: launch_gemv_pro<EPI, 3, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 4: launch_gemv_pro<EPI, 4, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
-    case 7:
-      if constexpr (EPI == PG_EPI_QKV_ROPE && FRAG) launch_gemv_pro<EPI, 7, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
-      break;
-    case 5:
-      if constexpr (EPI == PG_EPI_F32_FIN || EPI == PG_EPI_F32) launch_gemv_pro<EPI, 5, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
-      break;
     default: launch_gemv_pro<EPI, 0, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
   }
 }
@@ -1675,8 +1423,7 @@ static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K
 
 static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
                      int M, int N, int K, int epi_flags, int ksplit, const float* aux, int aux_rows, void* aux_out,
-                     int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream,
-                     const AttnArgs* att = nullptr, int att_total = 0, int* sync = nullptr) {
+                     int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
   const bool frag = (epi_flags & PG_W_FRAG) != 0;
   const bool fp8 = (epi_flags & PG_FP8) != 0;
   const bool m1 = (epi_flags & PG_TILE_M1) != 0;
@@ -1691,31 +1438,15 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
-  if (g_gemv_stamps && M <= 16 && f.pro_mode != 5)
-    e.stamps = g_gemv_stamps + (size_t)(g_gemv_launch++ % 128) * 2048 * 2;
-  if (f.pro_mode == 5) {
-    PG_REQUIRE(att != nullptr && sync != nullptr && att_total > 0 && f.asplit <= 16 && M <= 2 &&
-               (epi == PG_EPI_F32_FIN || epi == PG_EPI_F32) && att->D <= 256);
-    e.att = *att;
-    e.att_total = att_total;
-    e.att_wgs = (att_total + PG_AO_SPLITS_PER_WG - 1) / PG_AO_SPLITS_PER_WG;
-    e.sync = sync;
-    PG_REQUIRE(e.att_wgs <= ((N + 15) / 16) * ksplit);            // attention roles are a prefix of the grid
-  } else {
-    PG_REQUIRE((f.pro_mode >= 0 && f.pro_mode <= 4) || f.pro_mode == 7);
-  }
-  // pro 7: the batch-1 decode q|k|v of the two-stream schedule (every weight chunk issued before the wait)
-  if (f.pro_mode == 7)
-    PG_REQUIRE(M == 1 && epi == PG_EPI_QKV_ROPE && frag && ksplit == 1 && K == 2048 && f.wait_cnt && f.exit_cnt &&
-               f.err && f.wait_target > 0);
-  if (f.pro_mode == 0 || f.pro_mode == 4 || f.pro_mode == 7) PG_REQUIRE(A != nullptr && lda >= K);
+  PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 4);
+  if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
   // (M > 4 runs two 16-row tiles per workgroup: the per-row entries are loaded 16 per lane)
-  if (f.pro_mode == 4 || f.pro_mode == 7) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
+  if (f.pro_mode == 4) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
                                   ((M <= 2 && f.ss_n <= 256 && (M == 1 || f.ss_n <= 128)) ||
                                    (M > 4 && M <= 16 && f.ss_n <= 64)));
   if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
   if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
-  if (f.pro_mode == 2 || f.pro_mode == 5)
+  if (f.pro_mode == 2)
     PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 && f.asplit > 0 &&
                f.q_per_kv > 0 && f.kv_heads > 0);
   if (epi == PG_EPI_QKV_ROPE) PG_REQUIRE(f.head_dim % 16 == 0 && f.cos_t && f.sin_t && f.pos && f.kc && f.vtc &&
@@ -1780,23 +1511,6 @@ extern "C" int pg_gemm(const void* A, int lda, const void* W, int ldw, const flo
                    nullptr, stream);
 }
 
-// Decode attention + o_proj in one launch (pro_mode 5): the split-KV attention of pg_attention (decode mode)
-// runs in the first workgroups of the o_proj GEMV, the others stream their weights meanwhile, then every
-// workgroup merges the partials of its K range (the pg_gemm_fused pro_mode 2 prologue) and multiplies.
-extern "C" int pg_attn_oproj(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const void* vt,
-                             long vt_bs, long vt_hs, long vt_ds, int B, const int* lkv_dev, int Hq, int Hkv, int D,
-                             float scale, int split_keys, int* sync, const void* W, int ldw, void* C, int ldc, int N,
-                             int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream) {
-  PG_REQUIRE(fused != nullptr && fused->pro_mode == 5 && B > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && D % 8 == 0 &&
-             split_keys % 32 == 0 && split_keys > 0 && fused->head_dim == D && fused->kv_heads == Hkv &&
-             fused->q_per_kv == Hq / Hkv && fused->part_o && fused->part_ml);
-  AttnArgs a{(const bf16_t*)q, q_rs, nullptr, 0, (const bf16_t*)k, k_bs, k_hs, k_rs, (const bf16_t*)vt, vt_bs, vt_hs,
-             vt_ds, nullptr, 0, 0, 1, 1, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys,
-             (float*)fused->part_o, (float*)fused->part_ml, 0};
-  return gemm_impl(nullptr, K, W, ldw, nullptr, C, ldc, B, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream,
-                   &a, B * Hkv * fused->asplit, sync);
-}
-
 // C = epilogue(sum_z part[z]) for a GEMM run as PG_EPI_F32 with ksplit slabs (bias was applied to slab 0)
 extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc, int M, int N, int epi,
                                 void* aux_out, int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
@@ -1830,156 +1544,4 @@ extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc,
 extern "C" int pg_gemm_fused(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
                              int M, int N, int K, int epi, int ksplit, const PgFusedArgs* fused, hipStream_t stream) {
   return gemm_impl(A, lda, W, ldw, bias, C, ldc, M, N, K, epi, ksplit, nullptr, 0, nullptr, 0, 0, fused, stream);
-}
-
-// --------------------------------------------------------------------------------------
-// Decode attention block: q|k|v GEMV (RMSNorm prologue, RoPE + KV append) -> split-KV attention -> merge + o_proj
-// GEMV + in-kernel split-K finalisation, as ONE launch (batch <= 2, head_dim 256).  Replaces the three launches of
-// GemmaAttention.forward's decode step (modeling_gemma.py:264-358).  Roles by workgroup index: [0, nq) the q|k|v
-// tile pairs, [nq, nq + na) the attention (4 splits per workgroup, one per wave), then the o_proj (tile, split)
-// workgroups.  A role waits only for lower roles, and the launch is refused unless the whole grid is co-resident
-// (occupancy x CUs; the attention role's registers make it one 256-thread workgroup per CU, so the grid is sized
-// to at most one per CU: q|k|v as tile pairs, o_proj unsplit), so no wait depends on a workgroup that has not been
-// dispatched.  Hand-offs (MI355X guide, inter-workgroup hand-off table row 1): producers store write-through,
-// drain vmcnt, then one relaxed agent-scope add per workgroup (q|k|v: sync[2]) or per wave (attention: sync[0]);
-// consumers poll with relaxed agent loads and read the handed-off bytes with write-through-readable loads.
-// What the launch buys: the attention issues its cached K/V block and the o_proj its weights while the q|k|v
-// GEMV still streams, and two kernel boundaries go.
-struct DecodeBlockArgs {
-  const bf16_t* xq;      // q|k|v input x' (pro 4) or null (pro 1: RMSNorm of the residual)
-  int lda;
-  const bf16_t* wqkv;
-  EpiArgs eq;            // q|k|v epilogue, pub = 1
-  AttnArgs att;          // FUSED decode splits
-  const bf16_t* wo;
-  EpiArgs eo;            // o_proj: pro 6, PG_EPI_F32_FIN
-  int K, Ko;             // q|k|v input width (hidden), o_proj input width (q heads x head_dim)
-  int nq, na, no_tiles, ko;
-  int* sync;             // [0] attention waves done, [1] o workgroups past the merge, [2] q|k|v tiles done, [3] err
-  unsigned long long* stamps;   // diagnostics only (pg_decode_block_stamps): [workgroup][4] wall-clock stamps
-};
-
-static unsigned long long* g_block_stamps = nullptr;
-// Diagnostics: record per workgroup of every later pg_decode_attn_block launch its start, the end of its wait
-// (or of its GEMV main loop), and its end (100 MHz wall clock) into buf [grid][4] u64; null turns it off.
-extern "C" int pg_decode_block_stamps(void* buf) {
-  g_block_stamps = (unsigned long long*)buf;
-  return 0;
-}
-
-template <int PROQ, int CQ, int CO>
-__global__ __launch_bounds__(256) void decode_attn_block_kernel(DecodeBlockArgs a) {
-  int bid = blockIdx.x;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  unsigned long long* stamp = a.stamps ? a.stamps + (size_t)blockIdx.x * 4 : nullptr;
-  if (stamp && threadIdx.x == 0) stamp[0] = wall_clock64();
-  if (bid < a.nq) {
-    gemv_body<PG_EPI_QKV_ROPE, 2, 2, PG_GEMV_D2, PROQ, true, CQ>(a.xq, a.lda, a.wqkv, a.K, a.K, a.eq,
-                                                                  GemvIdx{bid, 0, a.nq, 1});
-    if (wave == 0) {   // wave 0 stored the tile write-through: drain, then arrive
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(a.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (stamp && lane == 0) stamp[2] = wall_clock64();
-    }
-    return;
-  }
-  bid -= a.nq;
-  if (bid < a.na) {
-    const int id = bid * 4 + wave;
-    if (id >= a.eo.att_total) return;
-    const int ns = a.eo.f.asplit;
-    const int sp = id % ns, kvh = (id / ns) % a.att.Hkv, b = id / (ns * a.att.Hkv);
-    attn_decode_split<256, 16, true, true, true>(a.att, b, kvh, sp, ns, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (stamp && threadIdx.x == 0) stamp[2] = wall_clock64();
-    return;
-  }
-  bid -= a.na;
-  gemv_body<PG_EPI_F32_FIN, 1, 2, 8, 6, true, CO>(nullptr, a.Ko, a.wo, a.Ko, a.Ko, a.eo,
-                                                  GemvIdx{bid % a.no_tiles, bid / a.no_tiles, a.no_tiles, a.ko});
-  if (stamp && threadIdx.x == 0) stamp[2] = wall_clock64();
-}
-
-template <int PROQ, int CQ, int CO>
-static int launch_decode_block(const DecodeBlockArgs& a, size_t lds, hipStream_t stream) {
-  // workgroups that can be resident at once: occupancy x CUs.  The occupancy API can answer one workgroup per CU
-  // too many when SGPRs bind (MI355X guide: residency), which only happens above two per CU: keep a margin there.
-  static int cap = -1;
-  if (cap < 0) {
-    int nb = 0, dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, decode_attn_block_kernel<PROQ, CQ, CO>, 256, 8192) !=
-            hipSuccess)
-      return (int)hipErrorNotSupported;
-    cap = (nb <= 2 ? nb : nb - 1) * cus;
-  }
-  const int grid = a.nq + a.na + a.no_tiles * a.ko;
-  if (grid > cap) return (int)hipErrorNotSupported;     // the caller runs the three-launch form instead
-  hipLaunchKernelGGL((decode_attn_block_kernel<PROQ, CQ, CO>), dim3(grid), dim3(256), lds, stream, a);
-  PG_LAUNCH_CHECK();
-  return 0;
-}
-
-// fq: the q|k|v GEMV's fused args (pro 1 or 4, RoPE / KV-cache fields; slot_dev = kv length before this token);
-// fo: the o_proj's (F32_FIN fields + the split-KV merge fields: part_o / part_ml / asplit <= 16 / akeys = keys per
-// split).  sync: 4 zeroed ints owned by the caller (self-resetting; sync[3] = 1 after a timed-out wait).
-// pub_k / pub_v: [M][Hkv * head_dim] bf16 scratch.  Returns hipErrorNotSupported (nothing launched) when the
-// grid cannot be co-resident on this device.
-extern "C" int pg_decode_attn_block(const void* xq, const void* wqkv, void* qbuf, const PgFusedArgs* fq,
-                                    const void* wo, float* oslab, const PgFusedArgs* fo, int ksplit_o, int M, int H,
-                                    void* pub_k, void* pub_v, int* sync, hipStream_t stream) {
-  PG_REQUIRE(fq && fo && wqkv && qbuf && wo && oslab && pub_k && pub_v && sync && M >= 1 && M <= 2);
-  PG_REQUIRE((fq->pro_mode == 1 && xq == nullptr && fq->resid_in && fq->norm_w && fq->nsplit == 0) ||
-             (fq->pro_mode == 4 && xq != nullptr && fq->ss_in && fq->ss_n > 0 && fq->ss_ld >= fq->ss_n &&
-              fq->ss_n <= 256 && (M == 1 || fq->ss_n <= 128)));
-  const int D = fq->head_dim, Hq = fq->q_heads, Hkv = fq->kv_heads;
-  PG_REQUIRE(D == 256 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && fq->cos_t && fq->sin_t && fq->pos &&
-             fq->kc && fq->vtc && fq->slot_dev && fq->rows_per_batch == 1 && fq->smax >= 32 && fq->smax % 32 == 0);
-  const int Nq = (Hq + 2 * Hkv) * D, Ko = Hq * D;
-  PG_REQUIRE(H % 256 == 0 && Ko % (256 * ksplit_o) == 0 && ksplit_o >= 1 && ksplit_o <= 8);
-  PG_REQUIRE(fo->fin_cnt && fo->fin_resid && fo->ss_out && fo->ss_ld >= H / 16 && fo->part_o && fo->part_ml &&
-             fo->asplit > 0 && fo->asplit <= 16 && fo->asplit % 4 == 0 && fo->head_dim == D && fo->kv_heads == Hkv &&
-             fo->q_per_kv == Hq / Hkv && fo->akeys == 32 && fo->asplit * 32 >= fq->smax &&
-             (fo->fin_x == nullptr || fo->norm_w != nullptr));
-  DecodeBlockArgs a{};
-  a.xq = (const bf16_t*)xq;
-  a.lda = H;
-  a.wqkv = (const bf16_t*)wqkv;
-  a.eq = EpiArgs{nullptr, qbuf, Ko, M, Nq, nullptr, 0, nullptr, 0, 0, *fq};
-  a.eq.pub = 1;
-  a.eq.pub_k = (bf16_t*)pub_k;
-  a.eq.pub_v = (bf16_t*)pub_v;
-  const int KV = Hkv * D, S = fq->smax;
-  a.att = AttnArgs{(const bf16_t*)qbuf, Ko, nullptr, 0, fq->kc, (long)S * KV, D, KV, fq->vtc, (long)KV * S, (long)D * S,
-                   S, nullptr, 0, 0, 1, 1, Hq / Hkv, Hkv, D, fq->slot_dev,
-                   (1.0f / sqrtf((float)D)) * 1.4426950408889634f, 32, (float*)fo->part_o, (float*)fo->part_ml, S,
-                   sync + 2, 0, (const bf16_t*)pub_k, (const bf16_t*)pub_v, sync + 3};
-  a.wo = (const bf16_t*)wo;
-  PgFusedArgs f6 = *fo;
-  f6.pro_mode = 6;
-  a.eo = EpiArgs{nullptr, oslab, H, M, H, nullptr, 0, nullptr, 0, 0, f6};
-  a.eo.att_total = M * Hkv * fo->asplit;
-  a.eo.sync = sync;
-  a.K = H;
-  a.Ko = Ko;
-  PG_REQUIRE(Nq % 32 == 0);
-  a.nq = Nq / 32;                                  // tile pairs
-  a.na = (a.eo.att_total + 3) / 4;
-  a.no_tiles = H / 16;
-  a.ko = ksplit_o;
-  a.att.wait_target = a.nq;
-  a.sync = sync;
-  a.stamps = g_block_stamps;
-  a.eo.stamps = g_block_stamps;
-  a.att.stamps = g_block_stamps;
-  // o_proj x staged in LDS by the merge prologue: M rows of this split's K range
-  const size_t lds = (((size_t)M * (Ko / ksplit_o + XPAD) * 2 + 15) & ~(size_t)15) + 64 * sizeof(float);
-  const int cq = H / 256, co = Ko / ksplit_o / 256;
-  if (fq->pro_mode == 4 && cq == 8 && co == 4) return launch_decode_block<4, 8, 4>(a, lds, stream);
-  if (fq->pro_mode == 1 && cq == 8 && co == 4) return launch_decode_block<1, 8, 4>(a, lds, stream);
-  if (fq->pro_mode == 4 && cq == 8 && co == 8) return launch_decode_block<4, 8, 8>(a, lds, stream);
-  if (fq->pro_mode == 1 && cq == 8 && co == 8) return launch_decode_block<1, 8, 8>(a, lds, stream);
-  return (int)hipErrorNotSupported;
 }

@@ -388,84 +388,6 @@ extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* works
   return 0;
 }
 
-// pg_argmax_embed in ONE launch: every (chunk, row) workgroup reduces its chunk as argmax_partial_kernel does and
-// stores the partial write-through, takes a ticket, and the grid's last workgroup runs argmax_final_embed_kernel's
-// reduction, state advance and embedding (4 waves over the rows).  Same winner, one launch and one kernel boundary
-// fewer per decode step.  The ticket is a device global (calls on different streams must not overlap).
-static __device__ int pg_am_ticket = 0;
-__global__ __launch_bounds__(256) void argmax_embed_onepass_kernel(const float* __restrict__ x, long ld, int V,
-                                                                   float* __restrict__ pv, int* __restrict__ pi,
-                                                                   int B, int64_t* __restrict__ out_ids,
-                                                                   int64_t* __restrict__ hist, int hist_rows,
-                                                                   int* __restrict__ step, int* __restrict__ pos,
-                                                                   int* __restrict__ kv_len, AmEmbArgs ea) {
-  __shared__ float sv[4];
-  __shared__ int si[4];
-  __shared__ int last;
-  __shared__ int win[AM_EMB_MAX_B];
-  const int b0 = blockIdx.y, ch = blockIdx.x;
-  {
-    const int per = ((V + AM_CHUNKS - 1) / AM_CHUNKS + 3) & ~3;
-    const int s = ch * per, e = min(V, s + per);
-    const float* row = x + (long)b0 * ld;
-    float bv = -INFINITY;
-    int bi = 0x7FFFFFFF;
-    for (int i = s + threadIdx.x * 4; i < e; i += 1024) {
-      if (i + 3 < e) {
-        const f32x4 v = *(const f32x4*)(row + i);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) am_better(bv, bi, v[j], i + j);
-      } else {
-        for (int j = 0; j < 4 && i + j < e; ++j) am_better(bv, bi, row[i + j], i + j);
-      }
-    }
-    am_block(bv, bi, sv, si);
-    if (threadIdx.x == 0) {
-      __hip_atomic_store((unsigned*)(pv + b0 * AM_CHUNKS + ch), __float_as_uint(bv), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(pi + b0 * AM_CHUNKS + ch, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      last = __hip_atomic_fetch_add(&pg_am_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (int)(gridDim.x * gridDim.y) - 1;
-    }
-  }
-  __syncthreads();
-  if (!last) return;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int st = step ? *step : 0;
-  for (int b = wave; b < B; b += nw) {
-    float bv = __uint_as_float(__hip_atomic_load((const unsigned*)(pv + b * AM_CHUNKS + lane), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT));
-    int bi = __hip_atomic_load(pi + b * AM_CHUNKS + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      float ov = __shfl_xor(bv, o, 64);
-      int oi = __shfl_xor(bi, o, 64);
-      am_better(bv, bi, ov, oi);
-    }
-    if (lane == 0) {
-      win[b] = bi;
-      out_ids[b] = bi;
-      if (hist && st < hist_rows) hist[(long)st * B + b] = bi;
-      if (pos) pos[b] += 1;
-    }
-  }
-  __syncthreads();                             // every wave has read *step and every winner is in LDS
-  if (threadIdx.x == 0) {
-    if (kv_len) *kv_len += 1;
-    if (step) *step = st + 1;
-    __hip_atomic_store(&pg_am_ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (int b = wave; b < B; b += nw) {
-    const int64_t id = win[b];
-    int rk = 0;
-    if (id == ea.image_id)
-      for (int i = 0; i < b; ++i) rk += win[i] == ea.image_id;
-    embed_row(ea.res + (long)b * ea.H, id, rk, lane, 64, ea.embed, ea.V, ea.feat, ea.n_feat, ea.H, ea.image_id,
-              ea.pad_id, ea.img_scale, ea.normalizer);
-  }
-}
-
 // pg_argmax + the next step's embedding rows (see argmax_final_embed_kernel); workspace as pg_argmax
 extern "C" int pg_argmax_embed(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
                                int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, const void* embed,
@@ -477,15 +399,6 @@ extern "C" int pg_argmax_embed(const float* logits, long ld, int B, int V, void*
   int* pi = (int*)(pv + B * AM_CHUNKS);
   const AmEmbArgs ea{(const bf16_t*)embed, V_embed, n_feat, H, feat, (int64_t)image_id, (int64_t)pad_id,
                      img_scale, normalizer, res};
-  // PG_ARGMAX_ONEPASS=1 (environment, tuning A/B): one launch, the ticketed last workgroup finishing -- neutral at
-  // batch 1, slower at batch 16 (its 4 waves run the final pass and the embedding of every row), so off
-  static const bool onepass = getenv("PG_ARGMAX_ONEPASS") && atoi(getenv("PG_ARGMAX_ONEPASS")) != 0;
-  if (onepass) {
-    hipLaunchKernelGGL(argmax_embed_onepass_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi, B,
-                       out_ids, hist, hist_rows, step, pos, kv_len, ea);
-    PG_LAUNCH_CHECK();
-    return 0;
-  }
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
   hipLaunchKernelGGL(argmax_final_embed_kernel, dim3(1), dim3(64 * am_waves(B)), 0, stream, pv, pi, B, out_ids, hist,
                      hist_rows, step, pos, kv_len, ea);
@@ -667,7 +580,25 @@ extern "C" int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, f
   return 0;
 }
 
-extern "C" int pg_abi_version(void) { return 3; }
+// ABI 4: the measured-slower decode variants removed (pg_attn_oproj, pg_decode_attn_block, pg_decode_mlp_block,
+// pg_decode_mlp_engine, pg_gateup_bank, pg_prefetch, the *_stamps diagnostics) and PgFusedArgs slimmed to the
+// fields the default path uses; pg_source_hash added.
+extern "C" int pg_abi_version(void) { return 4; }
+
+// sha256 (hex) over the csrc/ sources, include/pghip.h and the compile flags this library was built from
+// (pghip/build.py passes it as PG_SOURCE_HASH): the loader compares it with the tree it runs from, so a stale
+// prebuilt library cannot pass for the sources next to it.  The marker prefix lets the build read it from the file.
+#ifndef PG_SOURCE_HASH
+#define PG_SOURCE_HASH "unknown"
+#endif
+__attribute__((used)) static const char pg_source_hash_str[] = "PGHIP_SOURCE_HASH=" PG_SOURCE_HASH;
+extern "C" int pg_source_hash(char* out, int n) {
+  const char* h = pg_source_hash_str + 18;
+  int i = 0;
+  for (; h[i] && i + 1 < n; ++i) out[i] = h[i];
+  if (n > 0) out[i] = 0;
+  return h[i] ? (int)hipErrorInvalidValue : 0;
+}
 
 // ---------------------------------------------------------------- image pre-processing (processing_paligemma.py:13-73)
 // PIL BICUBIC resize of an RGB uint8 image (Pillow Resample.c, 22-bit fixed point, coefficient tables from

@@ -26,28 +26,15 @@ class PgFusedArgs(C.Structure):
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
                 ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
-                ("slab_rows", C.c_int), ("done_cnt", C.c_void_p), ("wait_cnt", C.c_void_p),
-                ("wait_target", C.c_int), ("exit_cnt", C.c_void_p), ("err", C.c_void_p)]
+                ("slab_rows", C.c_int)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
 SIGNATURES = {
     "pg_abi_version": [],
+    "pg_source_hash": [C.c_char_p, i32],
     "pg_gemm": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp],
     "pg_gemm_fused": [vp, i32, vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, C.POINTER(PgFusedArgs), vp],
-    "pg_attn_oproj": [vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, i32, vp, i32, i32, i32, f32, i32, vp, vp, i32,
-                      vp, i32, i32, i32, i32, i32, C.POINTER(PgFusedArgs), vp],
-    "pg_decode_attn_block": [vp, vp, vp, C.POINTER(PgFusedArgs), vp, vp, C.POINTER(PgFusedArgs), i32, i32, i32, vp, vp,
-                             vp, vp],
-    "pg_decode_block_stamps": [vp],
-    "pg_decode_mlp_stamps": [vp],
-    "pg_decode_mlp_engine": [vp, vp, i32, f32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, i32, vp],
-    "pg_decode_mlp_engine_stamps": [vp],
-    "pg_gateup_bank": [vp, vp, i32, f32, vp, vp, vp, i32, vp, vp, i32, i32, i32, vp],
-    "pg_gateup_bank_stamps": [vp],
-    "pg_gemv_stamps": [vp],
-    "pg_decode_mlp_block": [vp, vp, i32, i32, f32, vp, vp, vp, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32,
-                            vp],
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
@@ -65,7 +52,6 @@ SIGNATURES = {
     "pg_topp_sample": [vp, i64, i32, i32, f32, f32, vp, vp, vp, i32, vp, vp, vp, vp, vp],
     "pg_image_preprocess": [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp, vp, vp],
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
-    "pg_prefetch": [vp, i64, i32, i32, vp],
     "pg_quant_fp8": [vp, i32, i32, i32, vp, i32, vp, vp],
     "pg_norm_residual_fp8": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_xgmi_buffer_bytes": [i32, i64, C.POINTER(C.c_long)],
@@ -85,7 +71,22 @@ class PgHipError(RuntimeError):
     pass
 
 
+ABI_VERSION = 4
+
+
+def source_hash(lib=None) -> str:
+    """The source hash compiled into the loaded library (pg_source_hash)."""
+    lib = load() if lib is None else lib
+    buf = C.create_string_buffer(80)
+    if lib.pg_source_hash(buf, 80) != 0:
+        raise PgHipError("pg_source_hash: buffer too small")
+    return buf.value.decode()
+
+
 def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libpghip.so.  The product library must match this tree: its ABI version and the source hash compiled
+    into it (pghip/build.py) are checked against include/pghip.h's ABI and the csrc/ sources next to it, so a stale
+    prebuilt library raises instead of running (PGHIP_LIB, a tuning build, skips the source check)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -97,6 +98,15 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = C.c_int
+    if lib.pg_abi_version() != ABI_VERSION:
+        raise PgHipError(f"{path}: ABI {lib.pg_abi_version()}, this package expects {ABI_VERSION}; rebuild it")
+    if not os.environ.get("PGHIP_LIB"):
+        from . import build
+        if os.path.isdir(build.CSRC):
+            want, got = build.source_hash(), source_hash(lib)
+            if want != got:
+                raise PgHipError(f"{path} was built from other sources (hash {got[:16]}, tree {want[:16]}): "
+                                 "rebuild it with `python -m pghip.build`")
     _lib = lib
     return lib
 

@@ -4,14 +4,24 @@
 
 Each csrc/*.hip is compiled to an object in parallel, then linked into
 pghip/libpghip.so next to this file (git-ignored, but it travels to the GPU box
-with the snapshot).  Rebuilds only when a source or header is newer than the
-library.
+with the snapshot).
+
+Staleness is decided by content, not mtimes: source_hash() is a sha256 over
+every csrc/ source and header, include/pghip.h and the compile configuration
+(hipcc, flags, arch).  The hash is compiled into the library (PG_SOURCE_HASH,
+read back with pg_source_hash / library_hash()), so a prebuilt library that
+does not match the tree next to it is rebuilt here and refused at load time
+(_lib.load(check=True)).  Objects live in a directory named after the hash of
+the compile configuration, so a change of arch or flags never relinks objects
+built for another target.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -20,26 +30,53 @@ PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 LIB = os.path.join(HERE, "libpghip.so")
-OBJ_DIR = os.path.join(PKG, "build", "obj")
+OBJ_ROOT = os.path.join(PKG, "build", "obj")
 ARCH = os.environ.get("PGHIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-I", CSRC, "-I", INCLUDE,
          "-Wno-pass-failed"]
+_MARK = b"PGHIP_SOURCE_HASH="
 
 
 def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
-    return any(os.path.getmtime(p) > t for p in deps)
+def _inputs():
+    return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(INCLUDE, "pghip.h")]
 
 
-def _compile(src: str, obj_dir: str = OBJ_DIR, defines=()) -> str:
+def _config_tag(defines=()) -> str:
+    return hashlib.sha256(" ".join([HIPCC, *FLAGS, *defines]).encode()).hexdigest()[:12]
+
+
+def source_hash(defines=()) -> str:
+    """sha256 over the sources, headers and compile configuration the library is built from."""
+    h = hashlib.sha256()
+    for p in _inputs():
+        h.update(os.path.relpath(p, os.path.dirname(PKG)).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join([HIPCC, *FLAGS, *defines]).encode())
+    return h.hexdigest()
+
+
+def library_hash(path: str = LIB):
+    """The PG_SOURCE_HASH compiled into a built library (read from the file, no load), or None."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    m = re.search(re.escape(_MARK) + rb"([0-9a-f]{64}|unknown)", data)
+    return m.group(1).decode() if m else None
+
+
+def _stale(defines=()) -> bool:
+    return library_hash() != source_hash(defines)
+
+
+def _compile(src: str, obj_dir: str, defines=()) -> str:
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -53,18 +90,22 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     the product library is always the default build at pghip/libpghip.so."""
     if out == LIB and not defines and not force and not _stale():
         return LIB
-    obj_dir = OBJ_DIR if out == LIB else os.path.join(OBJ_DIR, os.path.basename(out).replace(".so", ""))
+    obj_dir = os.path.join(OBJ_ROOT, _config_tag(defines))
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
     # incremental: a source is recompiled when it, or any csrc header, is newer than its object (gemm.hip alone
-    # takes minutes; include/pghip.h is the C-ABI declaration, included by no source); a tuning variant (defines)
-    # always compiles everything
+    # takes minutes; include/pghip.h is the C-ABI declaration, included by no source).  misc.hip carries the
+    # source hash and is always recompiled.
     hdr = max([os.path.getmtime(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] or [0.0])
+    shash = source_hash(defines)
+    hash_def = f'PG_SOURCE_HASH="{shash}"'
 
     def obj_for(src):
         obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-        if (defines or force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr)):
+        if os.path.basename(src) == "misc.hip":
+            return _compile(src, obj_dir, (*defines, hash_def))
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
             return _compile(src, obj_dir, defines)
         return obj
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
@@ -76,7 +117,8 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, out)
     if verbose:
-        print(f"[pghip] built {out} from {len(srcs)} sources for {ARCH}" + (f" {list(defines)}" if defines else ""))
+        print(f"[pghip] built {out} from {len(srcs)} sources for {ARCH} (source hash {shash[:16]})"
+              + (f" {list(defines)}" if defines else ""))
     return out
 
 

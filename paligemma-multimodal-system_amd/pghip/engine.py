@@ -34,7 +34,7 @@ from typing import Optional
 import torch
 
 from . import ops
-from .tp import SoloComm
+from .tp import CaptureUnsupported, SoloComm
 from .weights import PackedWeights
 
 
@@ -92,36 +92,9 @@ class PaliGemmaEngine:
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
-    FUSE_ATTN_O = False     # with USE_FIN: the split-KV attention inside the o_proj launch (pg_attn_oproj): correct,
-                            # measured 1.31 vs 1.19 ms/token (the fused GEMV drops to 1 wave/SIMD; 252 pollers)
-    # with USE_FIN, B <= FUSE_MAX_B: q|k|v + attention + o_proj of a layer as ONE launch (pg_decode_attn_block)
-    # correct (bit-exact vs the three launches) but measured slower: 28.2 vs 16.5 us per layer on MI355X -- the
-    # in-launch hand-offs (2.7 us q|k|v -> attention, ~1 us attention -> o_proj) cost more than the two kernel
-    # boundaries they remove, so it is off
-    FUSE_BLOCK = os.environ.get("PG_FUSE_BLOCK", "0") == "1"
-    BLOCK_SPLIT_O = int(os.environ.get("PG_BLOCK_SPLIT_O", "1"))   # o_proj split-K inside the block launch
-    # with USE_FIN, B <= FUSE_MAX_B: gate/up + down of a layer as ONE launch (pg_decode_mlp_block; the down
-    # projection split (I/16)/(H/16) = 8 ways, its weights issued while the h hand-off is in flight)
-    MLP_BLOCK = os.environ.get("PG_MLP_BLOCK", "0") == "1"
-    # B = 1: gate/up + down as one persistent loader / consumer launch (pg_decode_mlp_engine, csrc/decode_engine.hip)
-    MLP_ENGINE = os.environ.get("PG_MLP_ENGINE", "0") == "1"
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
-    # tuning A/B (read by the library too): the batch-1 down projection as tile pairs, so its per-tile sums of
-    # squares come one per pair
-    FIN_NT2 = os.environ.get("PG_FIN_NT2", "0") not in ("", "0")
-    # B = 1, single rank: two-stream decode layers (_decode_layers_bank) -- the gate/up GEMV (pg_gateup_bank) and
-    # the down projection run on a side stream, each gate/up launched when the previous down ends so it loads half
-    # its weights on-chip while the q|k|v -> attention -> o_proj chain runs; the q|k|v GEMV likewise issues its
-    # weights before the down projection's hand-off (pro_mode 7).  The streams meet through done counters only.
-    DECODE_BANK = os.environ.get("PG_DECODE_BANK", "0") == "1"
-    # keys per attention split in that mode: 64 = two 32-key waves merged in LDS (attn_decode_wg_kernel, 236
-    # registers), so an attention wave fits on a SIMD beside a resident gate/up wave
-    BANK_SPLIT_KEYS = int(os.environ.get("PG_BANK_SK", "64"))
-    # tuning A/B: 0 = the next layer's q|k|v waits for the down projection through a stream dependency (a per-layer
-    # cross-queue edge) instead of in-kernel (pro_mode 7)
-    BANK_QKV_WAIT = os.environ.get("PG_BANK_QKV_WAIT", "1") != "0"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -146,11 +119,6 @@ class PaliGemmaEngine:
         self._rope_n = 0
         self._ws = {}
         self.graphs = {}
-        self._block_ok = True      # pg_decode_attn_block accepted by this device (else the three-launch form)
-        self._mlp_ok = True        # pg_decode_mlp_block accepted by this device (else the two-launch form)
-        self._engine_ok = True     # pg_decode_mlp_engine accepted by this device
-        self._bank_ok = True       # pg_gateup_bank accepted by this device
-        self._side = None          # side stream of the two-stream decode layers
 
     # ------------------------------------------------------------------ helpers
     def _buf(self, name, shape, dtype):
@@ -533,21 +501,6 @@ class PaliGemmaEngine:
             self.sample(logits, st, sampler, advance=True, feats=feats)
         return logits
 
-    def check(self):
-        """Raise if a fused decode launch gave up waiting inside the launch (its outputs are then invalid)."""
-        sync = self._ws.get("d_block_sync")
-        if sync is not None and int(sync[3].item()):
-            raise RuntimeError("pg_decode_attn_block: an in-launch wait timed out")
-        sync = self._ws.get("d_en_sync")
-        if sync is not None and int(sync[128].item()):
-            raise RuntimeError("pg_decode_mlp_engine: an in-launch wait timed out")
-        sync = self._ws.get("d_mlp_sync")
-        if sync is not None and int(sync[576].item()):
-            raise RuntimeError("pg_decode_mlp_block: an in-launch wait timed out")
-        err = self._ws.get("d_bank_err")
-        if err is not None and int(err[0].item()):
-            raise RuntimeError("two-stream decode: a cross-stream wait timed out")
-
     def _split_o(self, B: int) -> int:
         if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
             return self.DECODE_SPLIT_O_SMALL
@@ -578,7 +531,6 @@ class PaliGemmaEngine:
         so, sd = self._split_o(B), self.split_down
         tiles = (H + 15) // 16
         n_ss = tiles if B <= 4 else (tiles + 1) // 2         # one entry per GEMV workgroup (M > 4: tile pairs)
-        n_ss_d = (tiles + 1) // 2 if self.FIN_NT2 and self.split_down > 1 else n_ss   # the down projection's
         merge_in_gemv = B <= self.FUSE_MAX_B
         attn = None if merge_in_gemv else self._buf("d_attn", (B, nh * hd), torch.bfloat16)
         cnt = self._zeros("d_fin_cnt", (tiles,), torch.int32)
@@ -587,168 +539,41 @@ class PaliGemmaEngine:
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
         SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
-        if self._bank_on(B) and SK == self.BANK_SPLIT_KEYS:
-            return self._decode_layers_bank(st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t,
-                                            SK, xq, ss_o, ss_d, cnt, tiles, n_ss)
-        block = (self.FUSE_BLOCK and merge_in_gemv and self._block_ok and w.frag and hd == 256 and SK == 32 and
-                 nsplit <= 16 and cache.Smax % 32 == 0)
-        if block:
-            pub_k = self._buf("d_pub_k", (B, kvd), torch.bfloat16)
-            pub_v = self._buf("d_pub_v", (B, kvd), torch.bfloat16)
-            sync = self._zeros("d_block_sync", (4,), torch.int32)
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                         q_heads=nh, kv_heads=nkv)
-            if block:
-                # q|k|v + attention + o_proj in one launch (pg_decode_attn_block)
-                if i == 0:
-                    fq = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
-                                        **rope)
-                else:
-                    fq = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
-                fo = ops.fused_args(part_o=part_o, part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt,
-                                    q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt,
-                                    fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq, norm_w=Lw["post_w"])
-                ok = ops.decode_attn_block(None if i == 0 else xq, Lw["qkv_w"], qb, fq, Lw["o_w"], part, fo,
-                                           ksplit_o=self.BLOCK_SPLIT_O, M=B, pub_k=pub_k, pub_v=pub_v, sync=sync)
-                if not ok:
-                    if i > 0:
-                        raise RuntimeError("pg_decode_attn_block refused a later layer of the same step")
-                    self._block_ok = False      # this device cannot hold the grid: the three launches from now on
-                    block = False
-                else:
-                    nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-                    self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
-                    continue
             if i == 0:      # the embedding rows are final: plain RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                     **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
+                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
-            fused = self.FUSE_ATTN_O and nsplit <= 16 and merge_in_gemv
-            if not fused:
-                ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                              cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
-                              B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                              scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                              part_ml=part_ml, kcap=cache.Smax)
-            if not merge_in_gemv:
+            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
+                          part_ml=part_ml, kcap=cache.Smax)
+            if merge_in_gemv:
+                fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                    head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
+                                    akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
+                                    norm_w=Lw["post_w"])
+                ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
+            else:
                 ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
                 fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
                                     norm_w=Lw["post_w"])
                 ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
-            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_INLINE if fused else ops.PRO_ATTN_COMBINE, part_o=part_o,
-                                part_ml=part_ml, asplit=nsplit, head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv,
-                                slot_dev=st["kv_len"], akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles,
-                                fin_x=xq, norm_w=Lw["post_w"])
-            if not merge_in_gemv:
-                pass
-            elif fused:   # attention computed by the first workgroups of the o_proj GEMV (one launch)
-                ops.attn_oproj(qb, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd, cache.vt[i], kvd * cache.Smax,
-                               hd * cache.Smax, cache.Smax, Lw["o_w"], part, fa, self._zeros("d_attn_sync", (4,),
-                               torch.int32), B=B, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                               scale=1.0 / math.sqrt(hd), split_keys=SK, epi=ops.EPI_F32_FIN | w.wflag, ksplit=so)
-            else:
-                ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
             self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
-        return xq, ss_d, tiles, n_ss_d
-
-    def _bank_on(self, B: int) -> bool:
-        w = self.w
-        return (self.DECODE_BANK and self._bank_ok and B == 1 and self.tp == 1 and self.USE_FIN and w.frag and
-                not self.fp8 and w.hidden == 2048 and w.inter == 16384 and not self.FUSE_BLOCK and
-                not self.MLP_ENGINE and not self.MLP_BLOCK and not self.FUSE_ATTN_O)
-
-    def _decode_layers_bank(self, st, cache, res, qb, h, part, part_o, part_ml, nsplit, dt, cos_t, sin_t, SK, xq,
-                            ss_o, ss_d, cnt, tiles, n_ss):
-        """_decode_layers_fin at B = 1 on two streams.  Main stream: q|k|v -> attention -> o_proj (F32_FIN, counts
-        its finalised tiles into done[l][0]).  Side stream: pg_gateup_bank (issued when the previous layer's down
-        ends: half its weights load while the main stream's chain runs; waits for done[l][0]) -> down (F32_FIN,
-        counts into done[l][2]).  The next layer's q|k|v is launched right after this o_proj, issues all its weights
-        and waits for done[l][2] (pro_mode 7).  Every cross-stream value is stored write-through before the count
-        and read with agent-scope loads; the counters re-arm themselves.  One fork at the start of the step and one
-        join at the end are the only stream dependencies, so the captured graph has no per-layer cross-queue edge.
-        Bit-identical to _decode_layers_fin with the same attention split."""
-        w = self.w
-        H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
-        kvd = nkv * hd
-        so, sd = self._split_o(1), self.split_down
-        nl = len(w.tl)
-        n_ss_d = (tiles + 1) // 2 if self.FIN_NT2 and sd > 1 else n_ss
-        # per layer: [0] o_proj tiles done, [1] gate/up workgroups past the wait, [2] down tiles done, [3] q|k|v
-        # workgroups past the wait -- each on a 256-byte line of its own
-        done = self._zeros("d_bank_cnt", (nl, 4, 64), torch.int32)
-        err = self._zeros("d_bank_err", (64,), torch.int32)
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        main, side = torch.cuda.current_stream(), self._side
-        side.wait_stream(main)
-        for i, Lw in enumerate(w.tl):
-            rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
-                        slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
-                        q_heads=nh, kv_heads=nkv)
-            if i == 0:      # the embedding rows are final (same stream): plain RMSNorm prologue
-                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
-                                    **rope)
-                ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
-            elif self.BANK_QKV_WAIT:
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD_WAIT, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6,
-                                    wait_cnt=done[i - 1, 2], wait_target=n_ss_d, exit_cnt=done[i - 1, 3], err=err,
-                                    **rope)
-                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
-            else:
-                main.wait_stream(side)
-                fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss_d, eps=1e-6, **rope)
-                ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=1)
-            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
-                          B=1, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                          part_ml=part_ml, kcap=cache.Smax)
-            fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
-                                head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
-                                akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
-                                norm_w=Lw["post_w"], done_cnt=done[i, 0])
-            ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=1, ksplit=so)
-            nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            with torch.cuda.stream(side):
-                if not ops.gateup_bank(xq, ss_o, Lw["gu_w"], h, done[i, 0], done[i, 1], err, wait_target=tiles):
-                    raise RuntimeError("pg_gateup_bank refused the Gemma-2B batch-1 shape")
-                fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w,
-                                    done_cnt=done[i, 2] if i + 1 < nl and self.BANK_QKV_WAIT else None)
-                ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=1, ksplit=sd)
-        main.wait_stream(side)
-        return xq, ss_d, tiles, n_ss_d
+        return xq, ss_d, tiles, n_ss
 
     def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
-        (x' of the next norm -> xq, its sums of squares -> ss_d).  One pg_decode_mlp_block launch at B <= FUSE_MAX_B
-        when the device holds its grid, else the two GEMV launches."""
+        (x' of the next norm -> xq, its sums of squares -> ss_d)."""
         w = self.w
-        if self.MLP_ENGINE and self._engine_ok and B == 1 and w.frag:
-            H, I = w.hidden, w.inter
-            hg = self._buf("d_en_h", (I // 2,), torch.int64)
-            slab = self._buf("d_en_slab", (2, H), torch.float32)
-            tk = self._zeros("d_en_cnt", (H // 16,), torch.int32)
-            sync = self._zeros("d_en_sync", (192,), torch.int32)
-            if ops.decode_mlp_engine(xq, ss_o, Lw["gu_w"], Lw["down_w"], hg, slab, tk, res, ss_d, sync, fin_x=xq,
-                                     norm_w=nxt_w):
-                return
-            self._engine_ok = False
-        if self.MLP_BLOCK and self._mlp_ok and B <= self.FUSE_MAX_B and w.frag:
-            H, I = w.hidden, w.inter
-            ks = (I // 16) // (H // 16) if (I // 16) % (H // 16) == 0 else 0
-            if 1 <= ks <= 8:
-                slab = self._buf("d_mlp_slab", (ks, B, H), torch.float32)
-                sync = self._zeros("d_mlp_sync", (640,), torch.int32)
-                if ops.decode_mlp_block(xq, ss_o, Lw["gu_w"], h, Lw["down_w"], slab, cnt, res, ss_d, sync, M=B,
-                                        ksplit=ks, fin_x=xq, norm_w=nxt_w):
-                    return
-            self._mlp_ok = False         # this shape / device: the two launches from now on
         fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
         ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
         fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
@@ -759,8 +584,6 @@ class PaliGemmaEngine:
         merge kernel) whole multiples of 32 such that B * splits stays near DECODE_SPLIT_TARGET -- fewer (O, m, l)
         partials to write and merge once the batch alone fills the chip."""
         SK = self.DECODE_SPLIT_KEYS
-        if self._bank_on(B):
-            return self.BANK_SPLIT_KEYS
         if B <= self.FUSE_MAX_B:
             return self.DECODE_SPLIT_KEYS_SMALL
         blocks = (Smax + SK - 1) // SK
@@ -863,9 +686,10 @@ class PaliGemmaEngine:
         if use_graph and self.comm.capturable:
             try:
                 step_fn = self._graph_step(st, cache, feats, sampler)
-            except RuntimeError:
-                # a collective that cannot be captured (e.g. an all-reduce larger than the xGMI exchange
-                # buffer): _graph_step restored the state before capturing, so run eager steps instead
+            except CaptureUnsupported:
+                # a collective that cannot be captured (an all-reduce larger than the xGMI exchange buffer):
+                # _graph_step restored the state before capturing and a failed capture runs nothing, so the
+                # eager steps start from the same state.  Any other error propagates.
                 torch.cuda.synchronize()
                 step_fn = None
         if step_fn is None:
@@ -880,7 +704,6 @@ class PaliGemmaEngine:
             step_fn()
             n += 1
         hist = st["hist"][:n].t().contiguous().cpu()
-        self.check()
         if hasattr(self.comm, "check"):
             self.comm.check()              # an xGMI exchange that timed out leaves meaningless sums: raise
         if stop_token is None:
@@ -906,15 +729,17 @@ class PaliGemmaEngine:
         res0 = self._ws["d_res_a"][: st["ids"].numel() * self.w.hidden].clone() if st.get("chain") else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            self.decode_step(st, cache, feats, sampler)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        for k, v in snap.items():
-            st[k].copy_(v)
-        st["hist"].copy_(hist0)
-        if res0 is not None:                        # the chained input rows the warm-up step overwrote
-            self._ws["d_res_a"][: res0.numel()].copy_(res0)
+        try:
+            with torch.cuda.stream(s):
+                self.decode_step(st, cache, feats, sampler)
+            torch.cuda.current_stream().wait_stream(s)
+        finally:                                    # restored even when the warm-up step raises
+            torch.cuda.synchronize()
+            for k, v in snap.items():
+                st[k].copy_(v)
+            st["hist"].copy_(hist0)
+            if res0 is not None:                    # the chained input rows the warm-up step overwrote
+                self._ws["d_res_a"][: res0.numel()].copy_(res0)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.decode_step(st, cache, feats, sampler)

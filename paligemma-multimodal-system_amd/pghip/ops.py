@@ -14,8 +14,7 @@ import torch
 from . import _lib
 
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN = range(8)
-PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD, PRO_ATTN_INLINE = range(6)
-PRO_X_RSTD_WAIT = 7     # pro 4 whose input comes from another stream (two-stream batch-1 decode)
+PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
 TILE_M1 = 0x400  # OR into epi: all 256..288 rows in one row tile (batch-1 prefill, include/pghip.h PG_TILE_M1)
@@ -165,103 +164,6 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
     return out
 
 
-HIP_ERROR_NOT_SUPPORTED = 801
-
-
-def decode_attn_block(xq, Wqkv, qbuf, fq, Wo, oslab, fo, *, ksplit_o: int, M: int, pub_k, pub_v, sync) -> bool:
-    """pg_decode_attn_block: a decode layer's q|k|v GEMV + split-KV attention + o_proj in one launch.  Returns False
-    (nothing launched) when the device cannot hold the whole grid at once; raises on any other error."""
-    _chk(Wqkv, torch.bfloat16, "Wqkv")
-    _chk(Wo, torch.bfloat16, "Wo")
-    _chk(sync, torch.int32, "sync")
-    rc = _lib.load().pg_decode_attn_block(_p(xq), _p(Wqkv), _p(qbuf), _lib.C.byref(fq), _p(Wo), _p(oslab),
-                                          _lib.C.byref(fo), ksplit_o, M, Wqkv.shape[1], _p(pub_k), _p(pub_v),
-                                          _p(sync), _s())
-    if rc == HIP_ERROR_NOT_SUPPORTED:
-        return False
-    if rc != 0:
-        raise _lib.PgHipError(f"pg_decode_attn_block failed: hip error {rc} ({_lib._err_string(rc)})")
-    return True
-
-
-def decode_mlp_block(xq, ss_in, Wgu, h, Wd, slab, fin_cnt, resid, ss_out, sync, *, M: int, ksplit: int,
-                     eps: float = 1e-6, fin_x=None, norm_w=None) -> bool:
-    """pg_decode_mlp_block: a decode layer's gate/up GEMV + down GEMV (split-K ksplit, finalised into resid) in one
-    launch.  ss_in / ss_out: [M][ld] per-tile sums of squares (ld = their row stride).  Returns False (nothing
-    launched) when the device cannot hold the whole grid at once; raises on any other error."""
-    _chk(Wgu, torch.bfloat16, "Wgu")
-    _chk(Wd, torch.bfloat16, "Wd")
-    _chk(sync, torch.int32, "sync")
-    _chk(fin_cnt, torch.int32, "fin_cnt")
-    H, I = Wd.shape
-    if Wgu.shape != (2 * I, H) or sync.numel() < 640 or slab.numel() < ksplit * M * H or h.numel() < M * I:
-        raise ValueError("pghip.decode_mlp_block: shapes do not match")
-    rc = _lib.load().pg_decode_mlp_block(_p(xq), _p(ss_in), ss_in.stride(0), H // 16, float(eps), _p(Wgu), _p(h),
-                                         _p(Wd), _p(slab), ksplit, _p(fin_cnt), _p(resid), _p(ss_out),
-                                         ss_out.stride(0), _p(fin_x), _p(norm_w), _p(sync), M, H, I, _s())
-    if rc == HIP_ERROR_NOT_SUPPORTED:
-        return False
-    if rc != 0:
-        raise _lib.PgHipError(f"pg_decode_mlp_block failed: hip error {rc} ({_lib._err_string(rc)})")
-    return True
-
-
-def decode_mlp_engine(xq, ss_in, Wgu, Wd, hgran, slab, fin_cnt, resid, ss_out, sync, *, eps: float = 1e-6,
-                      fin_x=None, norm_w=None) -> bool:
-    """pg_decode_mlp_engine: a batch-1 decode layer's gate/up + down GEMVs as one persistent loader / consumer
-    launch (one workgroup per CU).  Returns False (nothing launched) for shapes or devices it does not cover."""
-    _chk(Wgu, torch.bfloat16, "Wgu")
-    _chk(Wd, torch.bfloat16, "Wd")
-    _chk(sync, torch.int32, "sync")
-    _chk(fin_cnt, torch.int32, "fin_cnt")
-    H, I = Wd.shape
-    if Wgu.shape != (2 * I, H) or sync.numel() < 192 or slab.numel() < 2 * H or hgran.numel() * hgran.element_size() < I * 4:
-        raise ValueError("pghip.decode_mlp_engine: shapes do not match")
-    rc = _lib.load().pg_decode_mlp_engine(_p(xq), _p(ss_in), H // 16, float(eps), _p(Wgu), _p(Wd), _p(hgran),
-                                          _p(slab), _p(fin_cnt), _p(resid), _p(ss_out), _p(fin_x), _p(norm_w),
-                                          _p(sync), 1, H, I, _s())
-    if rc == HIP_ERROR_NOT_SUPPORTED:
-        return False
-    if rc != 0:
-        raise _lib.PgHipError(f"pg_decode_mlp_engine failed: hip error {rc} ({_lib._err_string(rc)})")
-    return True
-
-
-def gateup_bank(xq, ss_in, Wgu, h, wait_cnt, exit_cnt, err, *, wait_target: int, eps: float = 1e-6) -> bool:
-    """pg_gateup_bank: the batch-1 decode gate/up GEMV (gelu(gate)*up) that loads half of its weights into
-    registers / LDS, then waits for *wait_cnt >= wait_target (an F32_FIN producer on another stream).  Returns
-    False (nothing launched) for shapes it does not cover."""
-    _chk(Wgu, torch.bfloat16, "Wgu")
-    for t, n in ((wait_cnt, "wait_cnt"), (exit_cnt, "exit_cnt"), (err, "err")):
-        _chk(t, torch.int32, n)
-    H = Wgu.shape[1]
-    I = Wgu.shape[0] // 2
-    if h.numel() < I or xq.numel() < H or ss_in.numel() < H // 16:
-        raise ValueError("pghip.gateup_bank: shapes do not match")
-    rc = _lib.load().pg_gateup_bank(_p(xq), _p(ss_in), H // 16, float(eps), _p(Wgu), _p(h), _p(wait_cnt),
-                                    int(wait_target), _p(exit_cnt), _p(err), 1, H, I, _s())
-    if rc == HIP_ERROR_NOT_SUPPORTED:
-        return False
-    if rc != 0:
-        raise _lib.PgHipError(f"pg_gateup_bank failed: hip error {rc} ({_lib._err_string(rc)})")
-    return True
-
-
-def attn_oproj(q, q_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, W, out, fa, sync, *, B, lkv_dev, Hq, Hkv, D,
-               scale, split_keys, epi, ksplit, N=None, ldc=None):
-    """pg_attn_oproj: split-KV decode attention computed inside the o_proj GEMV launch (fa.pro_mode = 5)."""
-    _chk(W, torch.bfloat16, "W")
-    _chk_frag(W, epi)
-    _chk(sync, torch.int32, "sync")
-    N = W.shape[0] if N is None else N
-    K = W.shape[1]
-    ldc = N if ldc is None else ldc
-    _lib.call("pg_attn_oproj", _p(q), q_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds, B, _p(lkv_dev),
-              Hq, Hkv, D, float(scale), split_keys, _p(sync), _p(W), W.stride(0), _p(out), ldc, N, K, epi, ksplit,
-              _lib.C.byref(fa), _s())
-    return out
-
-
 def norm_residual(resid: torch.Tensor, w: torch.Tensor, *, b: Optional[torch.Tensor] = None,
                   mode: int = NORM_RMS, eps: float = 1e-6, partials: Optional[torch.Tensor] = None,
                   nsplit: int = 0, out: Optional[torch.Tensor] = None, out_f32: Optional[torch.Tensor] = None,
@@ -386,14 +288,6 @@ def synth_fill(out: torch.Tensor, seedmix: int, a: float, mean: float):
     if kind == 1:
         _chk(out, torch.float32, "out")
     _lib.call("pg_synth_fill", _p(out), out.numel(), seedmix & 0xFFFFFFFF, float(a), float(mean), kind, _s())
-
-
-def prefetch(t: torch.Tensor, wgs: int = 256, policy: int = 0, nbytes: Optional[int] = None):
-    """Read t's bytes (or its first nbytes) into the Infinity Cache ahead of the kernel that streams them."""
-    if not t.is_cuda:
-        raise RuntimeError("pghip: prefetch needs a HIP tensor")
-    n = t.numel() * t.element_size() if nbytes is None else nbytes
-    _lib.call("pg_prefetch", _p(t), n - n % 16, wgs, policy, _s())
 
 
 _FIN_EPIS = (EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_BF16_VT, EPI_QKV_ROPE)

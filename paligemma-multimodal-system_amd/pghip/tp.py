@@ -14,6 +14,10 @@ from __future__ import annotations
 import torch
 
 
+class CaptureUnsupported(RuntimeError):
+    """A collective that cannot run inside a hipGraph capture (PaliGemmaEngine.generate then runs eager steps)."""
+
+
 class TPComm:
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -87,7 +91,7 @@ class XgmiComm(TPComm):
                            torch.cuda.current_stream().cuda_stream)
         else:
             if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError(f"XgmiComm: all-reduce of {t.numel()} x {t.dtype} does not fit the exchange "
+                raise CaptureUnsupported(f"XgmiComm: all-reduce of {t.numel()} x {t.dtype} does not fit the exchange "
                                    f"buffer (cap {self.cap} fp32) inside a graph capture")
             super().all_reduce(t)
 

@@ -127,13 +127,6 @@ class PackedWeights:
         for i in range(self.v_layers):
             lp = f"{pre}encoder.layers.{i}."
             a = lp + "self_attn."
-            for nm in ("q_proj.bias", "k_proj.bias", "v_proj.bias", "o_proj.bias"):
-                try:
-                    b = get(a + nm)
-                except KeyError:
-                    continue
-                if b is not None:
-                    raise NotImplementedError(f"{a + nm}: Gemma attention biases are not supported by the HIP path")
             qkv_w = torch.cat([bf(get(a + "query_proj.weight")), bf(get(a + "key_proj.weight")),
                                bf(get(a + "value_proj.weight"))], 0).contiguous()
             qkv_b = torch.cat([f32(get(a + "query_proj.bias")), f32(get(a + "key_proj.bias")),
@@ -216,7 +209,7 @@ class PackedWeights:
             for nm in ("q_proj.bias", "k_proj.bias", "v_proj.bias", "o_proj.bias"):
                 try:
                     b = get(a + nm)
-                except KeyError:
+                except LookupError:         # KeyError / IndexError of a mapping-style loader: the key is absent
                     continue
                 if b is not None:
                     raise NotImplementedError(f"{a + nm}: Gemma attention biases are not supported by the HIP path")

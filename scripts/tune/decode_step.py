@@ -22,7 +22,6 @@ ap.add_argument("--split-keys", type=int, default=None)
 ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--split-target", type=int, default=None)
 ap.add_argument("--fp8", action="store_true")
-ap.add_argument("--no-fuse-ao", action="store_true", help="attention as its own kernel (not inside o_proj)")
 a = ap.parse_args()
 
 from pghip import configs, engine, synthetic, weights  # noqa: E402
@@ -39,8 +38,6 @@ if a.split_keys:
     eng.DECODE_SPLIT_KEYS = a.split_keys
 if a.split_target:
     eng.DECODE_SPLIT_TARGET = a.split_target
-if a.no_fuse_ao:
-    eng.FUSE_ATTN_O = False
 B = a.batch
 ids, px = bench.synthetic_inputs(cfg, B, [2, 651, 4906, 603, 476, 2121, 576, 108])
 ids, px = ids.cuda(), px.cuda()
@@ -65,6 +62,6 @@ for rnd in range(5):
     times.append(e0.elapsed_time(e1) / a.steps)
 ids_out = st["hist"][: a.steps + 1, 0].tolist()
 print(json.dumps({"lib": os.path.basename(os.environ.get("PGHIP_LIB", "libpghip.so")), "split_o": eng.split_o,
-                  "split_down": eng.split_down, "split_keys": eng.DECODE_SPLIT_KEYS, "fuse_ao": eng.FUSE_ATTN_O, "B": B,
+                  "split_down": eng.split_down, "split_keys": eng.DECODE_SPLIT_KEYS, "B": B,
                   "ms_per_token": round(sorted(times)[2], 4), "all": [round(t, 4) for t in times],
                   "ids16": ids_out[:16]}), flush=True)

@@ -84,16 +84,15 @@ def test_chained_embed_generation_matches_unchained(tiny, golden, B):
     assert all(o == outs[0] for o in outs[1:])
 
 
-@pytest.mark.parametrize("fuse_max_b,use_fin,attn_o", [(2, True, True), (2, True, False), (2, False, False),
-                                                        (0, True, False)])
-def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin, attn_o):
+@pytest.mark.parametrize("fuse_max_b,use_fin", [(2, True), (2, False), (0, True)])
+def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin):
     """Long decode (no EOS stop) with the oracle's greedy continuation: per-step logits.  Layer forms:
-    in-kernel split-K finalisation with the attention inside the o_proj launch (default, single rank) or as
-    its own kernel, split-K partials reduced by the next GEMV's RMSNorm prologue (the TP form), and the
-    unfused layer (fuse_max_b=0, the B > 2 path)."""
+    in-kernel split-K finalisation with the split-KV merge in the o_proj prologue (default, single rank),
+    split-K partials reduced by the next GEMV's RMSNorm prologue (the TP form), and the unfused layer
+    (fuse_max_b=0, the B > 2 path)."""
     from oracle import paligemma_oracle as O
     eng, orc = tiny
-    eng.FUSE_MAX_B, eng.USE_FIN, eng.FUSE_ATTN_O = fuse_max_b, use_fin, attn_o
+    eng.FUSE_MAX_B, eng.USE_FIN = fuse_max_b, use_fin
     g = golden("tiny")
     ids_np = g["b1_input_ids"]
     steps = 24
@@ -111,30 +110,7 @@ def test_tiny_teacher_forced_decode_vs_oracle(tiny, golden, fuse_max_b, use_fin,
         top = np.sort(ref_logits[t][0])[::-1]
         if top[0] - top[1] > 0.1:
             assert int(st["ids"][0]) == ref_ids[t], t
-    eng.FUSE_MAX_B, eng.USE_FIN, eng.FUSE_ATTN_O = type(eng).FUSE_MAX_B, type(eng).USE_FIN, type(eng).FUSE_ATTN_O
-    if attn_o:
-        assert int(eng._ws["d_attn_sync"][2]) == 0 and int(eng._ws["d_attn_sync"][0]) == 0   # no give-up, reset
-
-
-def test_attn_oproj_matches_separate_launches(tiny, golden):
-    """pg_attn_oproj (attention inside the o_proj launch) == attention kernel + merge-prologue o_proj:
-    identical greedy tokens and logits over 10 steps (same partials, same merge order)."""
-    eng, _ = tiny
-    g = golden("tiny")
-    ids = torch.from_numpy(g["b1_input_ids"]).cuda()
-    px = torch.from_numpy(g["b1_pixel_values"]).cuda()
-    outs = []
-    for fused in (True, False):
-        eng.FUSE_ATTN_O = fused
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 12)
-        st = eng.decode_state(1, cache, nxt, 12)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(10)]
-        outs.append((st["hist"][:11, 0].tolist(), torch.stack(lg)))
-    eng.FUSE_ATTN_O = type(eng).FUSE_ATTN_O
-    assert outs[0][0] == outs[1][0]
-    assert err(outs[0][1].cpu().numpy(), outs[1][1].cpu().numpy()) < 1e-5
-    assert int(eng._ws["d_attn_sync"][2]) == 0
+    eng.FUSE_MAX_B, eng.USE_FIN = type(eng).FUSE_MAX_B, type(eng).USE_FIN
 
 
 @pytest.mark.slow
@@ -324,164 +300,3 @@ def test_tiny_batched_decode_fin_path_vs_oracle(tiny, golden, B):
         finally:
             eng.USE_FIN = type(eng).USE_FIN
     assert err(outs[True].cpu().numpy(), outs[False].cpu().numpy()) < 5e-3
-
-
-@pytest.mark.slow
-def test_pt224_fused_decode_block_bit_exact(golden):
-    """pg_decode_attn_block (a layer's q|k|v GEMV + split-KV attention + o_proj as ONE launch, q and the new k / v
-    handed over write-through inside the launch) against the three launches with the same o_proj split (1):
-    bit-identical logits, tokens and KV cache over 12 decode steps at full size (head_dim 256), no timed-out
-    wait, every in-launch counter back at zero; then the graph-replayed fused step reproduces the same tokens."""
-    from pghip import configs, engine, synthetic, weights
-    g = golden("pt224")
-    cfg = configs.PT_224
-    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
-    ids = torch.from_numpy(g["input_ids"]).cuda()
-    px = torch.from_numpy(g["pixel_values"]).cuda()
-    runs = []
-    for fused in (True, False):
-        eng.FUSE_BLOCK, eng.split_o, eng.DECODE_SPLIT_O_SMALL = fused, 1, 1
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
-        st = eng.decode_state(1, cache, nxt, 16)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
-        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
-    assert eng._block_ok
-    assert runs[0][0] == runs[1][0]
-    assert torch.equal(runs[0][1], runs[1][1])
-    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
-    sync = eng._ws["d_block_sync"]
-    assert int(sync[3]) == 0 and int(sync[:3].abs().sum()) == 0
-    eng.FUSE_BLOCK, eng.split_o = type(eng).FUSE_BLOCK, type(eng).DECODE_SPLIT_O
-    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
-    eng.DECODE_SPLIT_O_SMALL = type(eng).DECODE_SPLIT_O_SMALL
-    assert out[0].tolist() == runs[0][0]
-    assert int(g["greedy_ids"][0]) == runs[0][0][0]
-
-
-@pytest.mark.slow
-@pytest.mark.parametrize("B", [1, 2])
-def test_pt224_mlp_block_bit_exact(golden, B):
-    """pg_decode_mlp_block (a layer's gate/up GEMV + down GEMV as ONE launch, h handed over write-through inside the
-    launch, the down projection split 8 ways) against the two launches with the same down split (8): bit-identical
-    logits, tokens and KV cache over 12 full-size decode steps, no timed-out wait, every in-launch counter back at
-    zero; then the graph-replayed step reproduces the same tokens."""
-    from pghip import configs, engine, synthetic, weights
-    g = golden("pt224")
-    cfg = configs.PT_224
-    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
-    ids = torch.from_numpy(g["input_ids"]).cuda().repeat(B, 1)
-    px = torch.from_numpy(g["pixel_values"]).cuda().repeat(B, 1, 1, 1)
-    runs = []
-    for block in (True, False):
-        eng.MLP_BLOCK, eng.split_down = block, 8
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
-        st = eng.decode_state(B, cache, nxt, 16)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
-        runs.append((st["hist"][:13].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
-    assert eng._mlp_ok
-    assert runs[0][0] == runs[1][0]
-    assert torch.equal(runs[0][1], runs[1][1])
-    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
-    sync = eng._ws["d_mlp_sync"]
-    assert int(sync[576]) == 0 and int(sync.abs().sum()) == 0
-    assert int(eng._ws["d_fin_cnt"].abs().sum()) == 0
-    eng.MLP_BLOCK, eng.split_down = type(eng).MLP_BLOCK, type(eng).DECODE_SPLIT_DOWN
-    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
-    assert out.tolist() == [[row[b] for row in runs[0][0]] for b in range(B)]
-    assert int(g["greedy_ids"][0]) == runs[0][0][0][0]
-
-
-@pytest.mark.slow
-def test_pt224_mlp_engine_matches_two_launches(golden):
-    """pg_decode_mlp_engine (a batch-1 layer's gate/up + down GEMVs as one persistent loader / consumer launch, h
-    handed over as tagged granules, the down projection in two k-halves) against the two GEMV launches: 12
-    full-size decode steps from the same prefill, per-step logits within 1e-2 of their scale (a different fp32
-    summation order and split), the same greedy ids, no timed-out wait, the tickets back at zero and the epoch
-    advanced once per launch; then the graph-replayed step reproduces the same ids."""
-    from pghip import configs, engine, synthetic, weights
-    g = golden("pt224")
-    cfg = configs.PT_224
-    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
-    ids = torch.from_numpy(g["input_ids"]).cuda()
-    px = torch.from_numpy(g["pixel_values"]).cuda()
-    runs = []
-    for on in (True, False):
-        eng.MLP_ENGINE = on
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
-        st = eng.decode_state(1, cache, nxt, 16)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
-        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg)))
-    assert eng._engine_ok
-    assert runs[0][0] == runs[1][0]
-    for t in range(12):
-        assert err(runs[0][1][t].cpu().numpy(), runs[1][1][t].cpu().numpy()) < 1e-2, t
-    sync = eng._ws["d_en_sync"]
-    assert int(sync[128]) == 0 and int(sync[64]) == 0 and int(sync[0]) == 12 * 18
-    assert int(eng._ws["d_en_cnt"].abs().sum()) == 0
-    eng.MLP_ENGINE = True
-    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
-    eng.MLP_ENGINE = type(eng).MLP_ENGINE
-    assert out[0].tolist() == runs[0][0]
-
-
-@pytest.mark.slow
-def test_pt224_two_stream_decode_bit_exact(golden):
-    """The two-stream batch-1 decode layers (_decode_layers_bank: pg_gateup_bank + down on a side stream, the
-    q|k|v GEMV waiting in-kernel for the down projection's done counter) against the one-stream five launches with
-    the same 64-key attention splits: 12 full-size decode steps from the same prefill give bit-identical logits,
-    greedy ids and KV cache, no timed-out wait and every counter re-armed to zero; then the graph-replayed
-    two-stream step (a captured graph with two parallel branches) reproduces the same ids."""
-    from pghip import configs, engine, synthetic, weights
-    g = golden("pt224")
-    cfg = configs.PT_224
-    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
-    ids = torch.from_numpy(g["input_ids"]).cuda()
-    px = torch.from_numpy(g["pixel_values"]).cuda()
-    runs = []
-    for on in (True, False):
-        eng.DECODE_BANK, eng.DECODE_SPLIT_KEYS_SMALL = on, eng.BANK_SPLIT_KEYS
-        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 16)
-        st = eng.decode_state(1, cache, nxt, 16)
-        eng.sample(logits, st, dict(do_sample=False), advance=False)
-        lg = [eng.decode_step(st, cache, feats, dict(do_sample=False)).clone() for _ in range(12)]
-        torch.cuda.synchronize()
-        runs.append((st["hist"][:13, 0].tolist(), torch.stack(lg), cache.k.clone(), cache.vt.clone()))
-    assert eng._bank_ok
-    assert runs[0][0] == runs[1][0]
-    assert torch.equal(runs[0][1], runs[1][1])
-    assert torch.equal(runs[0][2], runs[1][2]) and torch.equal(runs[0][3], runs[1][3])
-    assert int(eng._ws["d_bank_err"].abs().sum()) == 0
-    assert int(eng._ws["d_bank_cnt"].abs().sum()) == 0
-    assert int(eng._ws["d_fin_cnt"].abs().sum()) == 0
-    eng.DECODE_BANK = True
-    out = eng.generate(ids, px, torch.ones_like(ids), 13, stop_token=None, use_graph=True)
-    assert int(eng._ws["d_bank_err"].abs().sum()) == 0
-    eng.DECODE_BANK, eng.DECODE_SPLIT_KEYS_SMALL = type(eng).DECODE_BANK, type(eng).DECODE_SPLIT_KEYS_SMALL
-    assert out[0].tolist() == runs[0][0]
-    assert int(g["greedy_ids"][0]) == runs[0][0][0]
-
-
-def test_gateup_bank_matches_gemv():
-    """pg_gateup_bank alone (its wait already satisfied) against pg_gemm_fused(gate/up, pro 4): the same h bits
-    for random fragment-packed Gemma-2B gate/up weights, x' and per-tile sums of squares; the counters re-arm."""
-    from pghip import ops, weights
-    torch.manual_seed(7)
-    H, I = 2048, 16384
-    w = (torch.randn(2 * I, H, device="cuda") * 0.02).to(torch.bfloat16)
-    wf = weights.frag_pack(w)
-    xq = torch.randn(1, H, device="cuda").to(torch.bfloat16)
-    ss = torch.rand(1, H // 16, device="cuda") * 10
-    h0 = torch.empty(1, I, dtype=torch.bfloat16, device="cuda")
-    fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss, ss_ld=H // 16, ss_n=H // 16, eps=1e-6)
-    ops.gemm_fused(xq, wf, h0, fa, epi=ops.EPI_BF16_GELU_MUL | ops.W_FRAG, M=1)
-    cnt = torch.tensor([H // 16], dtype=torch.int32, device="cuda")
-    ex = torch.zeros(1, dtype=torch.int32, device="cuda")
-    er = torch.zeros(1, dtype=torch.int32, device="cuda")
-    h1 = torch.empty_like(h0)
-    assert ops.gateup_bank(xq, ss, wf, h1, cnt, ex, er, wait_target=H // 16)
-    torch.cuda.synchronize()
-    assert int(er) == 0 and int(cnt) == 0 and int(ex) == 0
-    assert torch.equal(h0, h1)

@@ -55,7 +55,15 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == 3
+    assert lib.pg_abi_version() == _lib.ABI_VERSION == 4
+
+
+def test_library_matches_source_tree():
+    """The library carries the hash of the sources it was built from (pghip/build.py), and it equals the hash of
+    this tree: a stale prebuilt libpghip.so cannot be the one the GPU suite loads (_lib.load refuses it)."""
+    from pghip import _lib, build
+    assert build.library_hash() == build.source_hash() == _lib.source_hash()
+    assert len(build.source_hash()) == 64
 
 
 def test_no_cpu_fallback():
