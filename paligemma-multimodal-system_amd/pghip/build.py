@@ -46,8 +46,14 @@ def _inputs():
     return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(INCLUDE, "pghip.h")]
 
 
+def _config() -> str:
+    """The compile configuration without its machine-specific include paths (the GPU box holds the tree elsewhere)."""
+    flags = [f for f in FLAGS if f not in (CSRC, INCLUDE)]
+    return " ".join([os.path.basename(HIPCC), *flags])
+
+
 def _config_tag(defines=()) -> str:
-    return hashlib.sha256(" ".join([HIPCC, *FLAGS, *defines]).encode()).hexdigest()[:12]
+    return hashlib.sha256(" ".join([_config(), *defines]).encode()).hexdigest()[:12]
 
 
 def source_hash(defines=()) -> str:
@@ -58,7 +64,7 @@ def source_hash(defines=()) -> str:
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join([HIPCC, *FLAGS, *defines]).encode())
+    h.update(" ".join([_config(), *defines]).encode())
     return h.hexdigest()
 
 
