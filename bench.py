@@ -217,26 +217,37 @@ class Runner:
             self.replay()
 
 
-def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
-    """The Gemma decoder tensor-parallel over every rank (q heads, gate/up columns and the
-    vocabulary split; decode-size all-reduces as pg_allreduce_xgmi one-shot peer stores over xGMI, larger ones on
-    RCCL): ONE batch-1 request of the same workload across all `world` GPUs (strong scaling of per-token
-    latency).  Reported beside the data-parallel `value`; any failure is reported, never raised."""
-    from pghip import engine, weights
+def tp_leg(spec, rank, world, dist, steps=2):
+    """One tensor-parallel run over the ranks [0, spec["tp"]) (q heads, gate/up columns and the
+    vocabulary split; SigLIP data-parallel over the images when the batch covers the ranks; decode-size
+    collectives as pg_allreduce_xgmi / pg_allgather_xgmi one-shot peer stores over xGMI, larger ones on RCCL),
+    timing `steps` requests of spec's workload.  Every rank of the world takes part in the phase agreements;
+    ranks outside the TP group idle.  Phases: communicator setup, engine build (local only: packing, no
+    collective), a first request (prefill + decode-graph capture), timed requests.  After each phase all ranks
+    agree on its outcome (MIN of an ok flag), so a failure on one rank stops every rank at the same point and no
+    rank waits in a collective its peers skipped.  Any failure is reported in the record, never
+    raised."""
+    from pghip import configs, engine, synthetic, weights
     from pghip.tp import XgmiComm
-    out = {"tp": world, "comm": "pg_allreduce_xgmi (decode) + RCCL (beyond its buffer)", "scaling": "strong",
-           "workload": "the same request (batch 1) split over all GPUs"}
-    comm = None
+    tp = spec["tp"]
+    cfg = configs.CONFIGS[spec["config"]]
+    B, T, fp8, sample = spec["batch"], spec["tokens"], spec.get("fp8", False), spec.get("sample", False)
+    out = {"tp": tp, "config": spec["config"], "batch": B, "tokens": T, "fp8": fp8,
+           "sampler": "top-p T=0.8 p=0.9 (uniforms seed 4321)" if sample else "greedy", "baseline": spec["baseline"],
+           "comm": "pg_allreduce_xgmi / pg_allgather_xgmi (decode), RCCL beyond the exchange buffer",
+           "scaling": "strong"}
+    member = rank < tp
+    group = dist.new_group(list(range(tp))) if tp < world else None     # every rank calls new_group
     state = {}
 
     def phase(name, fn):
-        # every rank runs the phase, then all agree on its outcome (MIN of an ok flag): a failure on one rank makes
-        # every rank stop here together, so no rank is left waiting in a later collective of a phase the others skipped
         err = None
         try:
-            fn()
+            if member:
+                fn()
         except Exception as e:  # noqa: BLE001 (reported in the JSON line)
             err = f"{name}: {type(e).__name__}: {e}"
+        torch.cuda.synchronize()
         ok = torch.tensor([0 if err else 1], device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if err:
@@ -246,40 +257,43 @@ def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
         return int(ok.item()) == 1
 
     def make_comm():
-        nonlocal comm
-        comm = XgmiComm()
-
-    def sanity():
-        # rank-dependent values summed exactly, no timeout, on every rank
-        t = torch.full((4096,), float(rank + 1), device="cuda")
-        comm.all_reduce(t)
+        state["comm"] = XgmiComm(group=group)
+        t = torch.full((4096,), float(rank + 1), device="cuda")     # rank-dependent values, summed exactly
+        state["comm"].all_reduce(t)
         torch.cuda.synchronize()
-        if not (int(comm.err.item()) == 0 and bool((t == world * (world + 1) / 2).all())):
+        if not (int(state["comm"].err.item()) == 0 and bool((t == tp * (tp + 1) / 2).all())):
             raise RuntimeError("xGMI sanity all-reduce gave a wrong sum or timed out")
 
     def build():
-        eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
-                                     comm=comm)
-        state["eng"] = eng
-        state["run"] = Runner(eng, ids[:1], px[:1], T, dict(do_sample=False), False, rank)
+        sd = synthetic.SyntheticStateDict(cfg)
+        state["eng"] = engine.PaliGemmaEngine(
+            cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=tp, fp8=fp8), comm=state["comm"])
+        ids, px = synthetic_inputs(cfg, B, PROMPT)
+        state["ids"], state["px"] = ids.cuda(), px.cuda()
+
+    def first():
+        if sample:
+            g = torch.Generator().manual_seed(4321)
+            sampler = dict(do_sample=True, temperature=0.8, top_p=0.9, uniforms=torch.rand(T + 1, B, generator=g).cuda())
+        else:
+            sampler = dict(do_sample=False)
+        state["run"] = Runner(state["eng"], state["ids"], state["px"], T, sampler, False, rank)
         state["run"].request()
         torch.cuda.synchronize()
-        comm.check()
-
-    def barrier():
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
+        state["comm"].check()
 
     def timed():
         run = state["run"]
-        barrier()
+        g = state["comm"]._dist
+        torch.cuda.synchronize()
+        g.barrier(group=group)
         t0 = time.perf_counter()
         for _ in range(steps):
             run.request()
-        barrier()
+        torch.cuda.synchronize()
+        g.barrier(group=group)
         el = torch.tensor([time.perf_counter() - t0], device="cuda")
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        g.all_reduce(el, op=g.ReduceOp.MAX, group=group)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         ev[0].record()
         run.prefill_run()
@@ -292,13 +306,17 @@ def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
         ev[1].record()
         torch.cuda.synchronize()
         dec = ev[0].elapsed_time(ev[1]) / (T - 1)
-        comm.check()
-        out.update(tokens_per_s=round(T * steps / el.item(), 2), ms_per_request=round(el.item() / steps * 1e3, 3),
-                   prefill_ms=round(pf_ms, 3), decode_ms_per_token=round(dec, 4), decode=run.graph_mode)
+        state["comm"].check()
+        L = state["ids"].shape[1]
+        out.update(tokens_per_s=round(B * T * steps / el.item(), 2), ms_per_request=round(el.item() / steps * 1e3, 3),
+                   prefill_ms=round(pf_ms, 3), decode_ms_per_token=round(dec, 4), decode=run.graph_mode,
+                   prefill_tflops=round(prefill_flops(cfg, B, L) / (pf_ms / 1e3) / 1e12, 2))
 
-    for name, fn in (("xgmi setup", make_comm), ("xgmi sanity", sanity), ("tp engine", build), ("tp timing", timed)):
+    for name, fn in (("xgmi setup", make_comm), ("tp engine build", build), ("first request", first),
+                     ("timed requests", timed)):
         if not phase(name, fn):
             break
+    comm = state.pop("comm", None)
     state.clear()
     if comm is not None:
         try:
@@ -307,6 +325,24 @@ def tp_curve(cfg, sd, ids, px, T, rank, world, dist, steps=2):
             pass
     torch.cuda.empty_cache()
     return out
+
+
+def tp_specs(world):
+    """The tensor-parallel legs of a multi-GPU bench run: the headline workload over all N GPUs (the TP curve),
+    BASELINE configs[3] (mix-224 = the pt-224 architecture, top-p, TP=2) and configs[4] (pt-896, batch 32, fp8
+    Gemma linears, TP=N: TP=8 on the 8-GPU node)."""
+    return {
+        "tp": dict(tp=world, config="pt-224", batch=1, tokens=128, baseline="BASELINE.json configs[1] workload over "
+                   f"{world} GPUs (strong scaling of the per-token latency)"),
+        "configs[3]": dict(tp=2, config="mix-224", batch=1, tokens=128, sample=True,
+                           baseline="BASELINE.json configs[3]: PaliGemma-3B-mix-224 top-p sampling, Gemma TP=2"),
+        "configs[4]": dict(tp=world, config="pt-896", batch=32, tokens=128, fp8=True,
+                           baseline=f"BASELINE.json configs[4]: PaliGemma-3B-pt-896 batch 32, fp8 MFMA, TP={world}"
+                                    + ("" if world == 8 else " (the config names TP=8)")),
+    }
+
+
+PROMPT = [2, 651, 4906, 603, 476, 2121, 576, 108]
 
 
 def main():
@@ -328,8 +364,9 @@ def main():
     ap.add_argument("--graph-prefill", action="store_true",
                     help="replay the prefill as one hipGraph (measured 0.96-0.97x of eager launches: off by default)")
     ap.add_argument("--no-tp-curve", action="store_true",
-                    help="with --gpus N > 1 and --parallel dp: skip the extra tensor-parallel run of one request over "
-                    "all N GPUs (reported as \"tp\" beside the data-parallel value)")
+                    help="with --gpus N > 1 and --parallel dp: skip the extra tensor-parallel legs (the headline request "
+                    "over all N GPUs, BASELINE configs[3] at TP=2 and configs[4] at TP=N), reported beside the "
+                    "data-parallel value")
     ap.add_argument("--sample", action="store_true", help="top-p sampling (T=0.8, p=0.9, uniforms seed 4321) "
                     "instead of greedy, as BASELINE configs[3]")
     args = ap.parse_args()
@@ -345,10 +382,13 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        from datetime import timedelta
+        # a bounded collective timeout: a rank stuck in a collective its peers never issue ends the job with an
+        # error after 10 minutes instead of holding the node
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timedelta(minutes=10))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timedelta(minutes=10))
 
     from pghip import configs, engine, synthetic, weights
     cfg = configs.CONFIGS[args.config]
@@ -366,8 +406,7 @@ def main():
     torch.cuda.synchronize()
     log(f"[bench] rank {rank}: weights generated+packed in {time.perf_counter() - t0:.1f}s "
         f"({eng.w.nbytes() / 1e9:.2f} GB)")
-    prompt = [2, 651, 4906, 603, 476, 2121, 576, 108]
-    ids_cpu, px_cpu = synthetic_inputs(cfg, B, prompt)
+    ids_cpu, px_cpu = synthetic_inputs(cfg, B, PROMPT)
     ids, px = ids_cpu.cuda(), px_cpu.cuda()
     mask = torch.ones_like(ids)
     L = ids.shape[1]
@@ -435,10 +474,13 @@ def main():
     kern_desc = f"gemv_kernel<GELU_MUL,2> (decode gate/up, 2x{eng.w.inter}x{eng.w.hidden} bf16)"
 
     comm_used = eng.comm
-    eng.check()                                # a fused-launch wait that gave up invalidates the run
-    tp_rec = None
+    tp_recs = None
     if world > 1 and tp == 1 and not args.no_tp_curve:
-        tp_rec = tp_curve(cfg, sd, ids, px, T, rank, world, dist)
+        # the data-parallel engine is freed first (the TP legs build their own)
+        del state, eng, run, request, prefill_run, replay, sd
+        torch.cuda.empty_cache()
+        comm_used = None
+        tp_recs = {name: tp_leg(spec, rank, world, dist) for name, spec in tp_specs(world).items()}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         del state, eng, run, request, prefill_run, replay
@@ -480,10 +522,10 @@ def main():
                          "kernel_avg_us": round(kern_s * 1e6, 2), "bytes_per_launch": kern_bytes},
             "cpu_baseline": cpu,
         }
-        if tp_rec is not None:
-            rec["tp"] = tp_rec
+        if tp_recs is not None:
+            rec.update(tp_recs)
         print(json.dumps(rec), flush=True)
-    if hasattr(comm_used, "check"):
+    if comm_used is not None and hasattr(comm_used, "check"):
         comm_used.check()                      # a timed-out exchange invalidates the run
     if dist is not None:
         dist.destroy_process_group()

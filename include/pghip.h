@@ -222,6 +222,11 @@ int pg_xgmi_ipc_close(void* p);
  * can be captured into a hipGraph; every rank must issue the same sequence of calls. */
 int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
                       unsigned* epochs, int* err, hipStream_t stream);
+/* All-gather in rank order over the same exchange: out[r*n + i] = rank r's in[i] (the vocabulary-parallel
+ * lm_head logits; replaces the zero-padded SUM that moved W x the bytes).  in != out, both
+ * 16-byte aligned; otherwise as pg_allreduce_xgmi, whose buffer and epochs it shares (calls may interleave). */
+int pg_allgather_xgmi(const float* in, long n, float* out, int rank, int world, void* const* peers, long cap,
+                      unsigned* epochs, int* err, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -21,6 +21,11 @@
 // calls.  Everything the kernel needs lives on the device (epoch counters included), so the call is
 // capturable into the decode hipGraph.
 //
+// pg_allgather_xgmi is the same exchange with a different step 3: instead of summing, every rank copies the W
+// slots out in rank order (out = [W][n]), so the vocabulary-parallel logits travel once per rank instead of
+// W times in a zero-padded SUM.  Both share the exchange buffer and the per-workgroup epochs, so calls of the
+// two may be interleaved freely.
+//
 // Waiting is bounded by the 100 MHz wall clock: a peer that never arrives sets err[0] and the kernel
 // finishes (its output is then meaningless) instead of hanging the device.
 #include <cstring>
@@ -37,10 +42,10 @@ struct XgPeers {
   void* p[PG_XG_MAXW];
 };
 
-template <int W>
-__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__ data, long n, int rank,
+template <int W, bool GATHER>
+__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(const float* __restrict__ data, long n, int rank,
                                                              XgPeers peers, long cap, unsigned* __restrict__ epochs,
-                                                             int* __restrict__ err) {
+                                                             int* __restrict__ err, float* __restrict__ out) {
   const int wg = blockIdx.x, tid = threadIdx.x;
   const unsigned e = epochs[wg] + 1u;
   __syncthreads();
@@ -82,15 +87,21 @@ __global__ __launch_bounds__(256) void allreduce_xgmi_kernel(float* __restrict__
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
 
-  // 3. sum the W slots in rank order (identical on every rank)
+  // 3. sum the W slots in rank order (identical on every rank), or copy them out in rank order
   const float* slots = (const float*)((const char*)peers.p[rank] + PG_XG_FLAG_BYTES) + (long)set * W * cap;
   for (long c0 = (long)wg * PG_XG_CHUNK; c0 < n; c0 += STRIDE) {
     const long c1 = c0 + PG_XG_CHUNK < n ? c0 + PG_XG_CHUNK : n;
     for (long i = c0 + 4 * tid; i < c1; i += 1024) {
-      f32x4 s = __builtin_nontemporal_load((const f32x4*)(slots + i));
+      if constexpr (GATHER) {
 #pragma unroll
-      for (int p = 1; p < W; ++p) s += __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
-      *(f32x4*)(data + i) = s;
+        for (int p = 0; p < W; ++p)
+          *(f32x4*)(out + (long)p * n + i) = __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
+      } else {
+        f32x4 s = __builtin_nontemporal_load((const f32x4*)(slots + i));
+#pragma unroll
+        for (int p = 1; p < W; ++p) s += __builtin_nontemporal_load((const f32x4*)(slots + (long)p * cap + i));
+        *(f32x4*)(out + i) = s;
+      }
     }
   }
 }
@@ -139,25 +150,26 @@ extern "C" int pg_xgmi_ipc_open(const void* handle64, void** out) {
 
 extern "C" int pg_xgmi_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
-// In-place SUM of data[0, n) over `world` ranks.  peers[r] = rank r's exchange buffer as mapped in this
-// process (peers[rank] = the local one), each pg_xgmi_buffer_bytes(world, cap) long; epochs = PG_XG_MAXWG
-// zero-initialised local u32 words owned by this communicator; err = one local int (set to 1 on a timeout).
-// n % 4 == 0, n <= cap, data 16-B aligned.  Every rank must issue the same sequence of calls.
-extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
-                                 unsigned* epochs, int* err, hipStream_t stream) {
-  PG_REQUIRE(data != nullptr && peers != nullptr && epochs != nullptr && err != nullptr);
+static int xgmi_launch(const float* data, long n, float* out, bool gather, int rank, int world, void* const* peers,
+                       long cap, unsigned* epochs, int* err, hipStream_t stream) {
+  PG_REQUIRE(data != nullptr && out != nullptr && peers != nullptr && epochs != nullptr && err != nullptr);
   PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && rank >= 0 && rank < world);
-  PG_REQUIRE(n > 0 && n % 4 == 0 && n <= cap && cap % 4 == 0 && ((uintptr_t)data & 15) == 0);
+  PG_REQUIRE(n > 0 && n % 4 == 0 && n <= cap && cap % 4 == 0 && ((uintptr_t)data & 15) == 0 &&
+             ((uintptr_t)out & 15) == 0);
   XgPeers pp = {};
   for (int r = 0; r < world; ++r) {
     PG_REQUIRE(peers[r] != nullptr && ((uintptr_t)peers[r] & 15) == 0);
     pp.p[r] = peers[r];
   }
   // always the full grid: every workgroup's epoch advances on every call (see the header)
-#define PG_XG_CASE(WW)                                                                                       \
-  case WW:                                                                                                   \
-    hipLaunchKernelGGL((allreduce_xgmi_kernel<WW>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n, rank, pp, \
-                       cap, epochs, err);                                                                    \
+#define PG_XG_CASE(WW)                                                                                         \
+  case WW:                                                                                                     \
+    if (gather)                                                                                                \
+      hipLaunchKernelGGL((allreduce_xgmi_kernel<WW, true>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n,  \
+                         rank, pp, cap, epochs, err, out);                                                     \
+    else                                                                                                       \
+      hipLaunchKernelGGL((allreduce_xgmi_kernel<WW, false>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n, \
+                         rank, pp, cap, epochs, err, out);                                                     \
     break;
   switch (world) {
     PG_XG_CASE(1)
@@ -172,4 +184,21 @@ extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void*
 #undef PG_XG_CASE
   PG_LAUNCH_CHECK();
   return 0;
+}
+
+// In-place SUM of data[0, n) over `world` ranks.  peers[r] = rank r's exchange buffer as mapped in this
+// process (peers[rank] = the local one), each pg_xgmi_buffer_bytes(world, cap) long; epochs = PG_XG_MAXWG
+// zero-initialised local u32 words owned by this communicator; err = one local int (set to 1 on a timeout).
+// n % 4 == 0, n <= cap, data 16-B aligned.  Every rank must issue the same sequence of calls.
+extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
+                                 unsigned* epochs, int* err, hipStream_t stream) {
+  return xgmi_launch(data, n, data, false, rank, world, peers, cap, epochs, err, stream);
+}
+
+// out[r * n + i] = rank r's in[i] for every rank r (all-gather in rank order); in / out 16-B aligned, not
+// overlapping; the rest as pg_allreduce_xgmi (same buffer, same epochs).
+extern "C" int pg_allgather_xgmi(const float* in, long n, float* out, int rank, int world, void* const* peers,
+                                 long cap, unsigned* epochs, int* err, hipStream_t stream) {
+  PG_REQUIRE(in != out);
+  return xgmi_launch(in, n, out, true, rank, world, peers, cap, epochs, err, stream);
 }

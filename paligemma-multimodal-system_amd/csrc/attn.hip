@@ -34,6 +34,9 @@
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
+#ifndef PG_FA_SMALL
+#define PG_FA_SMALL 1     // prefill grids that leave most CUs idle at 4 waves (batch 1): 1- or 2-wave workgroups
+#endif
 
 // Decode (split mode): one wave per (batch, kv head, split); grid (1, Hkv * nsplit, B).
 template <int DP, int DT, bool FULL>
@@ -697,6 +700,10 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
   }
   if (waves == 8)
     hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 1>), grid, dim3(512), 0, stream, a);
+  else if (waves == 2)
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 2, 1>), grid, dim3(128), 0, stream, a);
+  else if (waves == 1)
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 1, 1>), grid, dim3(64), 0, stream, a);
   else
     hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 4, 1>), grid, dim3(256), 0, stream, a);
 }
@@ -772,6 +779,10 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
       // head_dim 256 (166 VGPRs, fits 3 waves / SIMD): 12 waves when the one-workgroup-per-CU rounds cost
       // less in total (pt-448 x16 Gemma: 688 workgroups in 3 rounds of 192 rows vs 1040 in 5 rounds of 128)
       if (PG_FA_W12 && DP == 256 && fa_waves == 8 && ((wgs(192) + 255) / 256) * 12 < ((wgs(128) + 255) / 256) * 8) fa_waves = 12;
+      // batch 1 (pt-224: Gemma 2112 stacked rows on one kv head = 33 four-wave workgroups, SigLIP 16 heads x 256
+      // rows = 64): narrower workgroups spread the same rows over 2-4x the CUs; each stages its own K / V^T copy
+      // from L2 (the whole prefix is a few hundred KB)
+      if (PG_FA_SMALL && fa_waves == 4 && wgs(64) < 256) fa_waves = wgs(32) >= 256 ? 2 : 1;
     }
     const int rows = 16 * fa_waves * fa_rpw;
     grid = dim3((Lq * G + rows - 1) / rows, Hkv, B);

@@ -61,6 +61,7 @@ SIGNATURES = {
     "pg_xgmi_ipc_open": [C.c_char_p, C.POINTER(C.c_void_p)],
     "pg_xgmi_ipc_close": [vp],
     "pg_allreduce_xgmi": [vp, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
+    "pg_allgather_xgmi": [vp, i64, vp, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
 }
 
 _lib = None

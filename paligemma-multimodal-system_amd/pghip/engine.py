@@ -20,10 +20,13 @@ the KV cache is a static in-place buffer instead of torch.cat (modeling_gemma.py
 the generation loop computes only last-position logits.
 
 Tensor parallelism (PackedWeights(tp_rank, tp_world) + a TPComm): every rank runs the same
-kernel sequence on its head / intermediate / vocabulary slice; partial sums of o_proj and
-down_proj are completed by one SUM all-reduce each (they already flow as split-K fp32
-partials, so the next RMSNorm prologue reduces them unchanged), greedy decoding combines
-per-rank (max, index) pairs, and full logits are assembled by a zero-padded all-reduce.
+kernel sequence on its head / intermediate / vocabulary slice.  The partial sums of o_proj and
+down_proj are completed by one SUM all-reduce of ONE fp32 slab per sub-block (a rank's split-K
+slabs are summed locally first); at prefill sizes the rows are cut into chunks and each chunk's
+all-reduce runs on the communication stream while the next chunk's GEMM runs (_row_parallel).
+Greedy decoding all-gathers per-rank (max, index) pairs, full logits are all-gathered by
+vocabulary slice, and with at least one image per rank the SigLIP tower runs data-parallel over
+the images, its features all-gathered.
 """
 from __future__ import annotations
 
@@ -92,6 +95,10 @@ class PaliGemmaEngine:
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
+    # tensor parallel: SigLIP data-parallel over the images when every rank gets at least one (else replicated)
+    VISION_DP = os.environ.get("PG_VISION_DP", "1") != "0"
+    # tensor-parallel prefill: rows per all-reduce chunk (each chunk's all-reduce overlaps the next chunk's GEMM)
+    AR_CHUNK_ROWS = int(os.environ.get("PG_AR_CHUNK_ROWS", "4096"))
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
@@ -141,13 +148,23 @@ class PaliGemmaEngine:
         return KVStore(w.t_layers, B, _rup(Smax, 64), w.kv_heads * w.head_dim, self.device)
 
     # ------------------------------------------------------------------ vision tower
-    def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False, taps: Optional[list] = None):
+    def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False, taps: Optional[list] = None,
+               _local: bool = False):
         """SiglipVisionModel.forward + projector (modeling_siglip.py:312-334, modeling_paligemma.py:60-65).
         Returns image features fp32 [B*N][P] (projector output, unscaled) and optionally the
         post-LN vision output fp32 [B*N][hv]."""
         w = self.w
         px = pixel_values.to(device=self.device, dtype=torch.float32).contiguous()
         B = px.shape[0]
+        if (not _local and self.tp > 1 and self.VISION_DP and B >= self.tp and B % self.tp == 0 and not want_hidden
+                and taps is None and w.proj_w is not None):
+            # data-parallel over the images (output-invariant, SURVEY.md §8(e)): this rank encodes its B/W images,
+            # then the projected features [B*N][P] are all-gathered in rank order = image order
+            Bl = B // self.tp
+            mine = self.vision(px[self.comm.rank * Bl:(self.comm.rank + 1) * Bl], _local=True)
+            feats = torch.empty(B * w.n_img, w.proj_dim, dtype=torch.float32, device=self.device)
+            self.comm.all_gather(feats, mine)
+            return feats
         N, hv, nh, hd = w.n_img, w.v_hidden, w.v_heads, w.v_head_dim
         M = B * N
         patches = self._buf("v_patches", (M, w.patch_k), torch.bfloat16)
@@ -233,13 +250,10 @@ class PaliGemmaEngine:
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
                           mask_rs=(mask.stride(-2) if mask is not None else 0))
-            self._lin(attn, Lw, "o", part, ops.EPI_F32, T, ksplit=s_o)
-            self._allreduce(part[:s_o])
-            xin = self._norm(x_resid, Lw["post_w"], part, s_o, xn, T)
+            n_o = self._row_parallel(attn, Lw, "o", part, T, s_o)
+            xin = self._norm(x_resid, Lw["post_w"], part, n_o, xn, T)
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
-            self._lin(h, Lw, "down", part, ops.EPI_F32, T, ksplit=s_d)
-            self._allreduce(part[:s_d])
-            ns = s_d
+            ns = self._row_parallel(h, Lw, "down", part, T, s_d)
             if taps is not None:
                 taps.append((x_resid + part[:ns].sum(0)).clone())
         cache.length = L
@@ -375,10 +389,35 @@ class PaliGemmaEngine:
         if self.tp > 1:
             self.comm.all_reduce(t)
 
+    def _row_parallel(self, x: torch.Tensor, Lw: dict, name: str, part: torch.Tensor, T: int, ks: int) -> int:
+        """A row-parallel prefill linear (o_proj / down_proj) into fp32 partial slabs; returns how many slabs the
+        next norm must add.  One rank: `ks` split-K slabs.  Tensor parallel: ONE slab, completed by a SUM all-reduce
+        -- a rank's split-K slabs are summed locally first (slab_sum), so every sub-block moves T*H*4 bytes instead
+        of ks times that.  From 2 * AR_CHUNK_ROWS rows on, the rows run as chunks with one split each: chunk c's
+        all-reduce is issued asynchronously (comm stream) and overlaps chunk c+1's GEMM."""
+        if self.tp == 1:
+            self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
+            return ks
+        C = T // self.AR_CHUNK_ROWS if T >= 2 * self.AR_CHUNK_ROWS else 1
+        if C <= 1:
+            self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
+            if ks > 1:
+                ops.slab_sum(part[:ks], part[0])
+            self.comm.all_reduce(part[0])
+            return 1
+        bounds = [T * c // C for c in range(C + 1)]
+        works = []
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            self._lin(x[r0:r1], Lw, name, part[0, r0:r1], ops.EPI_F32, r1 - r0, ksplit=1)
+            works.append(self.comm.all_reduce_async(part[0, r0:r1]))
+        for wk in works:
+            wk.wait()
+        return 1
+
     def lm_head(self, xf: torch.Tensor, rows: int, fresh: bool = False, name: str = "lm"):
         """Full-vocabulary logits fp32 [rows][V] from normalised bf16 rows (modeling_gemma.py:530-534).
-        Under TP each rank computes its vocabulary slice into its slot of a zeroed [rows][W][V/W]
-        buffer and a SUM all-reduce assembles the rows (exact: every other slot adds 0)."""
+        Under TP each rank computes its vocabulary slice and an all-gather assembles the rows (each slice
+        crosses the links once; the zero-padded SUM of round 2 moved W times the bytes)."""
         w = self.w
         alloc = (lambda shape: torch.empty(*shape, dtype=torch.float32, device=self.device)) if fresh else \
             (lambda shape: self._buf(name, shape, torch.float32))
@@ -386,12 +425,14 @@ class PaliGemmaEngine:
             logits = alloc((rows, w.vocab_local_pad))      # lm_w rows padded to 16 (fragment packing)
             ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
             return logits[:, :w.vocab]
-        vl, vlp = w.vocab_local, w.vocab_local_pad                       # 16-byte aligned slots
-        g = alloc((rows, self.tp, vlp))
-        g.zero_()
-        ops.gemm(xf, w.lm_w, g[:, self.comm.rank], epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias, M=rows)  # pad rows give 0
-        self._allreduce(g)
-        return g.view(rows, w.vocab) if vlp == vl else g[:, :, :vl].reshape(rows, w.vocab)
+        vl, vlp = w.vocab_local, w.vocab_local_pad
+        loc = self._buf(name + "_loc", (rows, vlp), torch.float32)
+        ops.gemm(xf, w.lm_w, loc, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
+        g = self._buf(name + "_gather", (self.tp, rows, vlp), torch.float32)
+        self.comm.all_gather(g, loc)                                      # [rank][rows][vocab slice]
+        out = alloc((rows, w.vocab))
+        out.view(rows, self.tp, vl).copy_(g[:, :, :vl].permute(1, 0, 2))
+        return out
 
     # ------------------------------------------------------------------ decode step (graph-capturable)
     def _chain_ok(self, sampler) -> bool:
@@ -489,10 +530,13 @@ class PaliGemmaEngine:
             loc = self._buf("d_logits_loc", (B, w.vocab_local_pad), torch.float32)
             ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
             loc = loc[:, :w.vocab_local]
-            pairs = self._buf("d_pairs", (self.tp, B, 2), torch.float32)
-            pairs.zero_()
-            ops.argmax_pairs(loc, st["ws"], pairs[self.comm.rank], vocab_offset=w.vocab_offset)
-            self._allreduce(pairs)
+            Bp = B + (B & 1)                    # whole 16-byte exchange units (pairs of rows)
+            mine = self._buf("d_pairs_loc", (Bp, 2), torch.float32)
+            ops.argmax_pairs(loc, st["ws"], mine, vocab_offset=w.vocab_offset)
+            pairs = self._buf("d_pairs", (self.tp, Bp, 2), torch.float32)
+            self.comm.all_gather(pairs, mine)
+            if Bp != B:
+                pairs = self._buf("d_pairs_b", (self.tp, B, 2), torch.float32).copy_(pairs[:, :B])
             ops.argmax_merge(pairs, st["ids"], world=self.tp, hist=st["hist"], step=st["step"], pos=st["pos"],
                              kv_len=st["kv_len"])
             return loc

@@ -1,13 +1,15 @@
 """Tensor-parallel communicator for the Gemma decoder.
 
-One process per GPU.  The only data-path collective is an in-place SUM all-reduce of
-fp32 partial sums — after o_proj, after down_proj, and for the vocabulary-parallel
-lm_head (each rank writes its slot of a zeroed buffer, so the SUM is an all-gather) —
-issued on the current HIP stream, either through torch.distributed (TPComm: backend
-"nccl" is RCCL over xGMI on the MI355X node, capturable into the decode hipGraph; "gloo"
-is the CPU transport used by the world-size-2 tests) or as the one-shot peer-store
-kernel pg_allreduce_xgmi (XgmiComm, csrc/allreduce.hip) for decode-size slabs.  The reference has no parallelism at all
-(single device, modeling_gemma.py / inference.py); this replaces nothing there.
+One process per GPU.  The data-path collectives are
+  * an in-place SUM all-reduce of fp32 partial sums after o_proj and after down_proj (row-parallel linears);
+  * an all-gather in rank order: the vocabulary-parallel lm_head logits (top-p / full logits) and, when the
+    batch covers the ranks, the SigLIP features of the images each rank encoded (data-parallel vision).
+They are issued on the current HIP stream, either through torch.distributed (TPComm: backend "nccl" is RCCL over
+xGMI on the MI355X node, capturable into the decode hipGraph; "gloo" is the CPU transport of the world-size-2
+tests) or as the one-shot peer-store kernels pg_allreduce_xgmi / pg_allgather_xgmi (XgmiComm,
+csrc/allreduce.hip) for decode-size messages.  all_reduce_async lets the prefill overlap a chunk's all-reduce
+with the next chunk's GEMM (the returned handle's wait() orders the current stream after the collective).  The
+reference has no parallelism at all (single device, modeling_gemma.py / inference.py); this replaces nothing there.
 """
 from __future__ import annotations
 
@@ -16,6 +18,21 @@ import torch
 
 class CaptureUnsupported(RuntimeError):
     """A collective that cannot run inside a hipGraph capture (PaliGemmaEngine.generate then runs eager steps)."""
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _StreamWork:
+    """A collective enqueued on a side stream: wait() makes the current stream wait for it."""
+
+    def __init__(self, event: torch.cuda.Event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
 
 
 class TPComm:
@@ -33,18 +50,29 @@ class TPComm:
     def all_reduce(self, t: torch.Tensor):
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
 
+    def all_reduce_async(self, t: torch.Tensor):
+        """SUM all-reduce that may run concurrently with later work on the current stream; call .wait() on the
+        result before the stream reads t."""
+        if self.backend == "gloo":                     # gloo stages device tensors through the host: synchronous
+            self.all_reduce(t)
+            return _Done()
+        return self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor):
+        """out (contiguous, world * t.numel() elements) = every rank's t in rank order."""
+        self._dist.all_gather_into_tensor(out.view(-1), t.contiguous().view(-1), group=self.group)
+
 
 class XgmiComm(TPComm):
-    """TP communicator whose decode-size all-reduces run as pg_allreduce_xgmi (one-shot peer stores over
-    xGMI, csrc/allreduce.hip); the process group only exchanges the IPC handles at construction and
+    """TP communicator whose decode-size collectives run as pg_allreduce_xgmi / pg_allgather_xgmi (one-shot peer
+    stores over xGMI, csrc/allreduce.hip); the process group only exchanges the IPC handles at construction and
     carries what does not fit (non-fp32, unaligned, or more than `cap` elements).
 
     Every rank holds one exchange buffer; the handles travel through all_gather_object, so this also
     works over gloo (two ranks sharing one device in the tests).  Because the kernel keeps its epoch
     counters on the device, the exchange is graph-capturable whatever the backend, so `capturable` is
-    True.  An all-reduce that does not fit the exchange buffer (`fits(numel)` False, e.g. the top-p
-    lm_head gather at a large batch) raises inside a capture; PaliGemmaEngine.generate and bench.py then
-    fall back to eager decode steps."""
+    True.  A collective that does not fit the exchange buffer (`fits(numel)` False) raises CaptureUnsupported
+    inside a capture; PaliGemmaEngine.generate and bench.py then fall back to eager decode steps."""
 
     def __init__(self, group=None, cap: int = 1 << 22):
         super().__init__(group)
@@ -77,23 +105,53 @@ class XgmiComm(TPComm):
         self._peers = peers
         self.epochs = torch.zeros(64, dtype=torch.int32, device="cuda")
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self._side = None
         self._dist.barrier(group=self.group)          # every rank mapped every buffer before first use
         self.capturable = True
 
     def fits(self, numel: int) -> bool:
         return 0 < numel <= self.cap and numel % 4 == 0
 
+    def _ok(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and self.fits(t.numel())
+                and t.data_ptr() % 16 == 0)
+
+    def _refuse_in_capture(self, what: str, t: torch.Tensor):
+        if torch.cuda.is_current_stream_capturing():
+            raise CaptureUnsupported(f"XgmiComm: {what} of {t.numel()} x {t.dtype} does not fit the exchange "
+                                     f"buffer (cap {self.cap} fp32) inside a graph capture")
+
     def all_reduce(self, t: torch.Tensor):
-        if (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and self.fits(t.numel())
-                and t.data_ptr() % 16 == 0):
+        if self._ok(t):
             self._lib.call("pg_allreduce_xgmi", t.data_ptr(), t.numel(), self.rank, self.world, self._peers,
                            self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
                            torch.cuda.current_stream().cuda_stream)
         else:
-            if torch.cuda.is_current_stream_capturing():
-                raise CaptureUnsupported(f"XgmiComm: all-reduce of {t.numel()} x {t.dtype} does not fit the exchange "
-                                   f"buffer (cap {self.cap} fp32) inside a graph capture")
+            self._refuse_in_capture("all-reduce", t)
             super().all_reduce(t)
+
+    def all_reduce_async(self, t: torch.Tensor):
+        if not self._ok(t):
+            return super().all_reduce_async(t)
+        # the exchange on a side stream that first waits for everything enqueued so far on the current one
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        self._side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._side):
+            self.all_reduce(t)
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+        return _StreamWork(ev)
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor):
+        t = t.contiguous()
+        if self._ok(t) and out.is_contiguous() and out.numel() == self.world * t.numel() and out.data_ptr() % 16 == 0:
+            self._lib.call("pg_allgather_xgmi", t.data_ptr(), t.numel(), out.data_ptr(), self.rank, self.world,
+                           self._peers, self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+        else:
+            self._refuse_in_capture("all-gather", t)
+            super().all_gather(out, t)
 
     def check(self):
         """Raise if any exchange timed out waiting for a peer (results since then are invalid)."""
@@ -118,3 +176,9 @@ class SoloComm:
 
     def all_reduce(self, t: torch.Tensor):
         return None
+
+    def all_reduce_async(self, t: torch.Tensor):
+        return _Done()
+
+    def all_gather(self, out: torch.Tensor, t: torch.Tensor):
+        out.view(-1).copy_(t.reshape(-1))

@@ -14,10 +14,11 @@ from pghip import build  # noqa: E402
 
 out, src, defs = sys.argv[1], sys.argv[2], sys.argv[3:]
 build.build()
-vdir = os.path.join(build.OBJ_DIR, "v_" + os.path.basename(out).replace(".so", ""))
+obj_dir = os.path.join(build.OBJ_ROOT, build._config_tag())
+vdir = os.path.join(obj_dir, "v_" + os.path.basename(out).replace(".so", ""))
 os.makedirs(vdir, exist_ok=True)
 obj = build._compile(os.path.join(build.CSRC, src), vdir, defs)
-objs = [o for o in sorted(glob.glob(os.path.join(build.OBJ_DIR, "*.o"))) if os.path.basename(o) != src + ".o"]
+objs = [o for o in sorted(glob.glob(os.path.join(obj_dir, "*.o"))) if os.path.basename(o) != src + ".o"]
 r = subprocess.run([build.HIPCC, f"--offload-arch={build.ARCH}", "-shared", "-fPIC", *objs, obj, "-o", out],
                    capture_output=True, text=True)
 if r.returncode:

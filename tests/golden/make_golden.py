@@ -15,7 +15,7 @@ Weights: oracle/synth.py's name-seeded bf16-exact synthetic tensors, loaded
 with the reference's own ``load_state_dict(strict=False)`` + ``tie_weights``
 (utils.py:33-36).
 
-Usage:  python tests/golden/make_golden.py [tiny] [pt224] [topp]
+Usage:  python tests/golden/make_golden.py [tiny] [pt224] [topp] [pt448] [pt896] [pt224wc]
 """
 from __future__ import annotations
 
@@ -214,6 +214,48 @@ def make_pt224(mp, inference, proc, steps=16):
     print("pt224: greedy", gen, "margins", np.round(out["margin"], 3))
 
 
+def make_large(mp, inference, proc, name, cfg, seeds, steps, row_stride, topk_k=64):
+    """BASELINE configs[2] / [4] sizes (pt-448: 1024 image tokens, pt-896: 4096) on the default synthetic weights:
+    one B=1 reference run per image (the reference's loop asserts batch 1, inference.py:69) through its own
+    test_inference, prefill + `steps` greedy tokens.  Images are regenerated from their seed (numpy PCG64,
+    stable across machines), so only the seed and the pixel-value checksums are stored.  Kept per image:
+    greedy ids, per-step top-k logits and top1-top2 margins, every `row_stride`-th row of the vision / projector
+    outputs, and per-layer statistics + last rows of the Gemma prefill."""
+    torch.set_num_threads(os.cpu_count())
+    model = build_reference_model(mp, cfg)
+    n = configs.num_image_tokens(cfg)
+    size = cfg["vision_config"]["image_size"]
+    out = {"seeds": np.array(seeds, dtype=np.int64), "row_stride": np.int64(row_stride)}
+    for j, seed in enumerate(seeds):
+        imgs = synthetic_images(1, size, seed)
+        pv = pixel_values_via_reference(proc, imgs)
+        ids = np.array([[cfg["image_token_index"]] * n + PROMPT_IDS], dtype=np.int64)
+        store, hs = capture_modules(model, cfg["text_config"]["num_hidden_layers"])
+        gen, logits = run_test_inference(inference, model, ids, pv, steps)
+        for h in hs:
+            h.remove()
+        lg = np.stack(logits, 0)[:, 0]
+        tv, ti = topk(lg, topk_k)
+        p = f"i{j}_"
+        out[p + "input_ids"] = ids
+        out[p + "pixel_sum"] = np.float64(pv.astype(np.float64).sum())
+        out[p + "pixel_sample"] = pv.reshape(-1)[:: 9973].copy()
+        out[p + "greedy_ids"] = np.array(gen, dtype=np.int64)
+        out[p + "step_top_values"] = tv
+        out[p + "step_top_ids"] = ti
+        out[p + "margin"] = tv[:, 0] - tv[:, 1]
+        out[p + "vision_rows"] = store["vision_out"][0, ::row_stride]
+        out[p + "proj_rows"] = store["proj_out"][0, ::row_stride]
+        for i in range(cfg["text_config"]["num_hidden_layers"]):
+            h = store[f"text_layer_{i}"][0]
+            out[p + f"layer_{i}_stats"] = np.array([h.mean(), np.abs(h).max(), np.sqrt((h.astype(np.float64) ** 2).sum())])
+            out[p + f"layer_{i}_last_row"] = h[-1]
+        out[p + "final_norm_last_row"] = store["text_final_norm"][0, -1]
+        print(f"{name} image {seed}: greedy", gen, "margins", np.round(out[p + "margin"], 3), flush=True)
+        del store
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+
+
 def make_topp(inference):
     rng = np.random.default_rng(7)
     cases = {}
@@ -246,7 +288,7 @@ def make_topp(inference):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["tiny", "topp", "pt224"]
+    which = sys.argv[1:] or ["tiny", "topp", "pt224", "pt448", "pt896"]
     mp, inference, proc = import_reference()
     torch.manual_seed(0)
     if "tiny" in which:
@@ -255,3 +297,7 @@ if __name__ == "__main__":
         make_topp(inference)
     if "pt224" in which:
         make_pt224(mp, inference, proc)
+    if "pt448" in which:          # BASELINE configs[2]: two images (the B=16 GPU test replicates each 8 times)
+        make_large(mp, inference, proc, "pt448", configs.PT_448, [1234, 1235], steps=8, row_stride=16)
+    if "pt896" in which:          # BASELINE configs[4]
+        make_large(mp, inference, proc, "pt896", configs.PT_896, [1234], steps=3, row_stride=64)

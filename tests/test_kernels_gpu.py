@@ -227,7 +227,9 @@ def _attn_ref(q, k, v, scale, mask=None):
 
 
 @pytest.mark.parametrize("B,N,nh,hd", [(1, 256, 16, 72), (2, 16, 8, 24), (1, 100, 4, 64),
-                                       (4, 256, 16, 72), (10, 104, 16, 72)])   # last two: LDS-staged kernel
+                                       (4, 256, 16, 72), (10, 104, 16, 72),     # LDS-staged kernel
+                                       (1, 1024, 16, 72), (16, 1024, 16, 72),  # pt-448 (B = 1, BASELINE configs[2])
+                                       (2, 4096, 16, 72)])                     # pt-896 (BASELINE configs[4])
 def test_attention_vision_layout(B, N, nh, hd):
     """SigLIP: q/k from the fused QKV buffer, V^T from the transposed side buffer.  Large batches take
     the LDS-staged kernel (>= 1024 sixteen-row groups), including a ragged last key block (N=104)."""
@@ -248,11 +250,14 @@ def test_attention_vision_layout(B, N, nh, hd):
 @pytest.mark.parametrize("B,L,nh,nkv,hd,masked", [(1, 264, 8, 1, 256, False), (2, 24, 4, 1, 32, True),
                                                   (1, 70, 8, 2, 64, False),
                                                   (8, 300, 8, 1, 256, False), (16, 130, 8, 1, 256, True),
-                                                  (14, 300, 8, 1, 256, False)])   # 12-wave flash kernel
+                                                  (14, 300, 8, 1, 256, False),    # 12-wave flash kernel
+                                                  (1, 1032, 8, 1, 256, False), (16, 1032, 8, 1, 256, False),  # pt-448
+                                                  (2, 4104, 8, 1, 256, False)])                              # pt-896
 def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
-    """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode."""
+    """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode, up to the pt-896 prefix
+    (4104 keys: the 2 / 4 / 8-block decode splits of BASELINE configs[4] over 4.2 k keys)."""
     from pghip import ops
-    Smax = 320
+    Smax = max(320, (L + 8 + 63) // 64 * 64)
     kvd = nkv * hd
     q = rnd(B * L, nh * hd, seed=11)
     kc = torch.zeros(B, Smax, kvd, dtype=torch.bfloat16, device="cuda")

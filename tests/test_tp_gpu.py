@@ -24,29 +24,32 @@ def _port():
         return s.getsockname()[1]
 
 
-def _launch(worker, tmp_path, **env):
+def _launch(worker, tmp_path, nproc=2, timeout=600, **env):
     env = dict(os.environ, TP_OUT=str(tmp_path), **env)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", worker)]
-    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
+    return [json.load(open(tmp_path / f"rank{i}.json")) for i in range(nproc)]
 
 
-def test_xgmi_allreduce_two_ranks_on_one_device(tmp_path):
-    """pg_allreduce_xgmi between two processes sharing the device through IPC-mapped exchange buffers:
-    bit-exact against the rank-order fp32 sum for ragged sizes (one and many workgroups, both buffer
-    sets), back to back with different sizes and no host sync, identical on both ranks, inside a captured
-    hipGraph, and without a timeout."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_allreduce_ranks_on_one_device(tmp_path, world):
+    """pg_allreduce_xgmi / pg_allgather_xgmi between `world` processes sharing the device through IPC-mapped
+    exchange buffers (the 8-rank case is the TP=8 exchange of BASELINE configs[4]): bit-exact against the
+    rank-order fp32 sum / concatenation for ragged sizes (one and many workgroups, both buffer sets), back to
+    back with different sizes and no host sync, all-gathers interleaved with all-reduces, identical on every
+    rank, inside a captured hipGraph, and without a timeout."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
-    res = _launch("xgmi_worker.py", tmp_path)
+    res = _launch("xgmi_worker.py", tmp_path, nproc=world)
     for o in res:
         assert o["err"] == 0, o
         assert o["bad"] == [], o
         assert o["graph_bad"] == [], o
         assert o["seq_bad"] == [], o
-    assert res[0]["digest"] == res[1]["digest"]
+        assert o["gather_bad"] == [], o
+    assert len({o["digest"] for o in res}) == 1
 
 
 @pytest.mark.parametrize("comm", ["gloo", "xgmi"])
@@ -63,3 +66,28 @@ def test_tp2_engine_on_one_device(tmp_path, comm):
         assert o["decode_argmax_agree"], o
         assert o["sampled_tp"] == o["sampled_solo"], o
     assert res[0]["greedy"] == res[1]["greedy"] and res[0]["sampled_tp"] == res[1]["sampled_tp"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("comm", ["gloo", "xgmi"])
+def test_tp2_full_size_pt224(tmp_path, comm):
+    """Full-size PaliGemma-3B-224 at TP=2 (BASELINE configs[3]: mix-224 top-p, which has the pt-224 architecture),
+    two ranks on one device.  Against the single-rank engine: prefill logits < 5e-3 scaled, every teacher-forced
+    decode step's gathered logits < 5e-3 (the partial sums are added in another order), the same top-1 wherever
+    the single-rank margin exceeds 0.05, and every top-p draw equal to the oracle's explicit-uniform inverse CDF
+    of the TP logits.  Against the reference (tests/golden/pt224.npz): the prefill top-1 and the top-64 logits
+    within the 15% intrinsic bf16 bound of test_pt224_full_size_teacher_forced_decode.  Free-running greedy and
+    top-p ids with fixed uniforms equal the single-rank engine's."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("tp_worker.py", tmp_path, timeout=900, TP_COMM=comm, TP_CFG="pt-224")
+    for o in res:
+        assert o["xgmi_err"] == 0, o
+        assert o["prefill_err_vs_solo"] < 5e-3, o
+        assert o["prefill_top1"] == o["ref_top1"], o
+        assert o["prefill_top64_err"] < 0.15, o
+        assert o["decode_err_vs_solo"] < 5e-3, o
+        assert o["decode_disagree"] == [], o
+        assert o["greedy_tp"] == o["greedy_solo"], o
+        assert o["sampled_tp"] == o["sampled_solo"], o
+    assert res[0]["greedy_tp"] == res[1]["greedy_tp"] and res[0]["sampled_tp"] == res[1]["sampled_tp"]

@@ -1,6 +1,8 @@
 """Rank body of tests/test_tp_gpu.py (launched by torch.distributed.run, 2 ranks on one HIP device,
-gloo transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden vectors and the
-single-rank engine.  Writes one JSON verdict per rank to $TP_OUT/rank<r>.json."""
+gloo transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden
+vectors and the single-rank engine.  TP_CFG=tiny (default) uses the tiny fixtures; TP_CFG=pt-224 runs the full-size
+PaliGemma-3B-224 (BASELINE configs[3]'s mix-224 architecture) against tests/golden/pt224.npz.  Writes one JSON
+verdict per rank to $TP_OUT/rank<r>.json."""
 import json
 import os
 import sys
@@ -24,6 +26,8 @@ def main():
     torch.cuda.set_device(0)
     from pghip import configs, engine, synthetic, weights
     from pghip.tp import TPComm, XgmiComm
+    if os.environ.get("TP_CFG", "tiny") != "tiny":
+        return full_size(rank, world, os.environ["TP_CFG"])
     cfg = configs.TINY
     sd = synthetic.SyntheticStateDict(cfg)
     comm = XgmiComm(cap=1 << 20) if os.environ.get("TP_COMM") == "xgmi" else TPComm()
@@ -71,6 +75,74 @@ def main():
     out["decode_argmax_agree"] = agree
     # top-p sampling with the same uniforms through the gathered logits
     u = torch.rand(9, 1, generator=torch.Generator().manual_seed(3))
+    out["sampled_tp"] = tp.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
+                                    stop_token=None)[0].tolist()
+    out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
+                                        stop_token=None)[0].tolist()
+    torch.cuda.synchronize()
+    out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+    if isinstance(comm, XgmiComm):
+        comm.close()
+    with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def full_size(rank, world, name):
+    """Full-size TP=2 (BASELINE configs[3]: mix-224 = the pt-224 architecture) on one device: prefill / teacher-forced
+    decode logits against the single-rank engine and the reference's golden, greedy ids, and top-p sampling with fixed
+    uniforms (the sampled ids must be the explicit-uniform inverse-CDF draw of the gathered logits)."""
+    from oracle import paligemma_oracle as O
+    from pghip import configs, engine, synthetic, weights
+    from pghip.tp import TPComm, XgmiComm
+    cfg = configs.CONFIGS[name]
+    sd = synthetic.SyntheticStateDict(cfg)
+    comm = XgmiComm() if os.environ.get("TP_COMM") == "xgmi" else TPComm()
+    tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
+                                comm=comm)
+    solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "pt224.npz")))
+    ids = torch.from_numpy(g["input_ids"]).cuda()
+    px = torch.from_numpy(g["pixel_values"]).cuda()
+    am = torch.ones_like(ids)
+    out = {"rank": rank, "world": world, "comm": type(comm).__name__, "graph": comm.capturable, "config": name}
+    steps = len(g["greedy_ids"])
+    res = []
+    for e in (tp, solo):
+        c, f, lg, n = e.prefill_request(ids, px, am, steps + 2)
+        res.append((c, f, lg.clone(), n))
+    out["prefill_err_vs_solo"] = err(res[0][2].cpu().numpy(), res[1][2].cpu().numpy())
+    out["prefill_top1"] = int(res[0][2][0].argmax())
+    out["ref_top1"] = int(g["greedy_ids"][0])
+    top_ids, top_v = g["step_top64_ids"][0], g["step_top64_values"][0]
+    out["prefill_top64_err"] = float(np.abs(res[0][2][0].cpu().numpy()[top_ids] - top_v).max() / np.abs(top_v).max())
+    # teacher-forced decode with the reference's ids: the full gathered logits (top-p sampler path) vs single rank
+    st = [e.decode_state(1, c, n, steps + 2) for e, (c, f, lg, n) in zip((tp, solo), res)]
+    worst, disagree = 0.0, []
+    samp = dict(do_sample=True, temperature=0.8, top_p=0.9)
+    for t in range(1, steps):
+        lgs = []
+        for e, s_, (c, f, lg, n) in zip((tp, solo), st, res):
+            s_["ids"].fill_(int(g["greedy_ids"][t - 1]))
+            s_["step"].zero_()
+            samp["uniforms"] = torch.full((4, 1), 0.5, device="cuda")
+            lgs.append(e.decode_step(s_, c, f, samp).clone())
+        a, b = lgs[0][0].cpu().numpy(), lgs[1][0].cpu().numpy()
+        worst = max(worst, err(a, b))
+        sb = np.sort(b)[::-1]
+        if sb[0] - sb[1] > 0.05 and int(a.argmax()) != int(b.argmax()):
+            disagree.append(t)
+        # the sampled id equals the oracle's explicit-uniform draw from the same (TP-gathered) logits
+        want = int(O.sample_top_p(a[None], 0.8, 0.9, np.array([0.5], np.float32))[0, 0])
+        if int(st[0]["ids"][0]) != want:
+            disagree.append(("topp", t, int(st[0]["ids"][0]), want))
+    out["decode_err_vs_solo"] = worst
+    out["decode_disagree"] = disagree
+    # free-running greedy (graph-captured when the communicator allows) and top-p with fixed uniforms
+    out["greedy_tp"] = tp.generate(ids, px, am, 8, stop_token=None)[0].tolist()
+    out["greedy_solo"] = solo.generate(ids, px, am, 8, stop_token=None)[0].tolist()
+    u = torch.rand(9, 1, generator=torch.Generator().manual_seed(4321))
     out["sampled_tp"] = tp.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
                                     stop_token=None)[0].tolist()
     out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,

@@ -32,7 +32,8 @@ def main():
     comm = XgmiComm(cap=1 << 20)
     bad, dig = [], hashlib.sha256()
     # ragged sizes: one workgroup, partial last chunk, many workgroups, the cap itself; each twice (both sets)
-    for it, n in enumerate([4, 1000, 8192, 8196, 2048 * 16, 257216, 3 * 8192 * 64 + 4, 1 << 20] * 2):
+    sizes = [4, 1000, 8192, 8196, 2048 * 16, 257216, 3 * 8192 * 64 + 4, 1 << 20] if world <= 2 else [4, 8196, 2048 * 16]
+    for it, n in enumerate(sizes * 2):
         t = rank_data(n, rank, it).cuda()
         comm.all_reduce(t)
         got = t.cpu()
@@ -49,6 +50,17 @@ def main():
         comm.all_reduce(t)
     torch.cuda.synchronize()
     seq_bad = [[n, i] for i, (n, t) in enumerate(zip(seq, ins)) if not torch.equal(t.cpu(), expected(n, world, 200 + i))]
+    # all-gather in rank order (pg_allgather_xgmi), interleaved with all-reduces on the same buffer / epochs
+    gather_bad = []
+    for it, n in enumerate([4, 2048, 32160, 8196, 1 << 20 if world <= 2 else 1 << 18]):
+        t = rank_data(n, rank, 300 + it).cuda()
+        out = torch.empty(world * n, device="cuda")
+        comm.all_gather(out, t)
+        r = rank_data(8, rank, 400 + it).cuda()
+        comm.all_reduce(r)
+        want = torch.cat([rank_data(n, q, 300 + it) for q in range(world)])
+        if not torch.equal(out.cpu(), want) or not torch.equal(r.cpu(), expected(8, world, 400 + it)):
+            gather_bad.append(n)
     # captured: three exchanges of different sizes in one graph, replayed with fresh inputs
     sizes = [2048, 2048 * 16, 4 * 8192]
     static = [torch.zeros(n, device="cuda") for n in sizes]
@@ -73,6 +85,7 @@ def main():
             if not torch.equal(t.cpu(), expected(n, world, it)):
                 graph_bad.append([n, rep])
     out = {"rank": rank, "err": int(comm.err.item()), "bad": bad, "graph_bad": graph_bad, "seq_bad": seq_bad,
+           "gather_bad": gather_bad,
            "digest": dig.hexdigest()}
     del g
     comm.close()
