@@ -21,7 +21,7 @@ product's HIP generator (``pghip.synthetic`` / ``pg_synth_fill``) implements
 the same formula; tests/test_synth.py checks that the two agree bit-for-bit and
 that their recipes agree for every key.
 
-The recipe is SURVEY.md §8(c)'s "measured-good" non-degenerate init (default
+The default recipe is SURVEY.md §8(c)'s "measured-good" non-degenerate init (default
 init makes greedy decode repeat one token): Linear W std 2/sqrt(fan_in),
 embeddings/pos/conv std 0.02, Gemma RMSNorm w std 0.1, LayerNorm w 1 + std 0.1,
 biases std 0.02, lm_head.bias std 1.
@@ -51,7 +51,7 @@ def seed_of(name: str) -> int:
     return int(fmix32(s)[0])
 
 
-def recipe(name: str, shape) -> tuple[float, float]:
+def recipe(name: str, shape, linear_gain: float = 2.0) -> tuple[float, float]:
     """(std, mean) for a reference state-dict key.  Mirrors pghip.synthetic.recipe."""
     if name.endswith(("layer_norm1.weight", "layer_norm2.weight", "post_layernorm.weight")):
         return 0.1, 1.0
@@ -64,7 +64,7 @@ def recipe(name: str, shape) -> tuple[float, float]:
     if name.endswith(".bias"):
         return 0.02, 0.0
     if len(shape) == 2:
-        return 2.0 / math.sqrt(shape[1]), 0.0
+        return linear_gain / math.sqrt(shape[1]), 0.0
     raise KeyError(f"no synthetic recipe for {name} {tuple(shape)}")
 
 
@@ -75,9 +75,9 @@ def bf16_round(x: np.ndarray) -> np.ndarray:
     return u.view(np.float32)
 
 
-def generate(name: str, shape, chunk: int = 1 << 24) -> np.ndarray:
+def generate(name: str, shape, chunk: int = 1 << 24, linear_gain: float = 2.0) -> np.ndarray:
     """The synthetic tensor for ``name`` (fp32 holding bf16-exact values)."""
-    std, mean = recipe(name, shape)
+    std, mean = recipe(name, shape, linear_gain)
     n = int(np.prod(shape))
     a = np.float32(std * math.sqrt(3.0))
     mean32 = np.float32(mean)
@@ -154,5 +154,8 @@ def state_dict_shapes(cfg: dict) -> dict:
     return shapes
 
 
-def generate_state_dict(cfg: dict) -> dict:
-    return {k: generate(k, s) for k, s in state_dict_shapes(cfg).items()}
+def generate_state_dict(cfg: dict, linear_gain: float = 2.0) -> dict:
+    """linear_gain: the 2-D Linear std is linear_gain / sqrt(fan_in).  2.0 (default) is the non-degenerate recipe
+    above; 1.6 is the better-conditioned one of tests/golden/pt224wc.npz (bf16 rounding grows ~5x less through the
+    45 layers, so the reference's greedy margins clear it and free-running ids can be compared exactly)."""
+    return {k: generate(k, s, linear_gain=linear_gain) for k, s in state_dict_shapes(cfg).items()}

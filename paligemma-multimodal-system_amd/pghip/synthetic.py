@@ -30,7 +30,7 @@ def seed_of(name: str) -> int:
     return _fmix32(zlib.crc32(name.encode("utf-8")) & 0xFFFFFFFF)
 
 
-def recipe(name: str, shape) -> tuple:
+def recipe(name: str, shape, linear_gain: float = 2.0) -> tuple:
     """(std, mean) per reference state-dict key (SURVEY.md §8(c) non-degenerate init)."""
     if name.endswith(("layer_norm1.weight", "layer_norm2.weight", "post_layernorm.weight")):
         return 0.1, 1.0
@@ -43,7 +43,7 @@ def recipe(name: str, shape) -> tuple:
     if name.endswith(".bias"):
         return 0.02, 0.0
     if len(shape) == 2:
-        return 2.0 / math.sqrt(shape[1]), 0.0
+        return linear_gain / math.sqrt(shape[1]), 0.0
     raise KeyError(f"no synthetic recipe for {name} {tuple(shape)}")
 
 
@@ -93,8 +93,8 @@ def state_dict_shapes(cfg: dict) -> dict:
     return s
 
 
-def generate(name: str, shape, device="cuda", dtype=torch.bfloat16) -> torch.Tensor:
-    std, mean = recipe(name, shape)
+def generate(name: str, shape, device="cuda", dtype=torch.bfloat16, linear_gain: float = 2.0) -> torch.Tensor:
+    std, mean = recipe(name, shape, linear_gain)
     out = torch.empty(shape, dtype=dtype, device=device)
     ops.synth_fill(out, seed_of(name), float(std * math.sqrt(3.0)), float(mean))
     return out
@@ -103,9 +103,11 @@ def generate(name: str, shape, device="cuda", dtype=torch.bfloat16) -> torch.Ten
 class SyntheticStateDict:
     """Lazy mapping key -> device tensor (bf16 for matrices, fp32 for vectors)."""
 
-    def __init__(self, cfg: dict, device="cuda"):
+    def __init__(self, cfg: dict, device="cuda", linear_gain: float = 2.0):
+        """linear_gain: 2-D Linear std = linear_gain / sqrt(fan_in) (oracle/synth.py generate_state_dict)."""
         self.shapes = state_dict_shapes(cfg)
         self.device = device
+        self.linear_gain = linear_gain
 
     def keys(self):
         return self.shapes.keys()
@@ -116,4 +118,4 @@ class SyntheticStateDict:
     def __getitem__(self, k):
         shape = self.shapes[k]
         dt = torch.bfloat16 if len(shape) >= 2 else torch.float32
-        return generate(k, shape, self.device, dt)
+        return generate(k, shape, self.device, dt, self.linear_gain)

