@@ -46,4 +46,22 @@ for rnd in range(3):
         gpu = ev[0].elapsed_time(ev[1]) / a.reps
         res.setdefault(f"{a.knob}={int(on)}", []).append([round(gpu, 3), round(host, 3)])
         print(f"{a.knob}={int(on)} prefill {gpu:.3f} ms (host issue {host:.3f} ms)", flush=True)
+# the same prefill replayed from one captured hipGraph (bench.py --graph-prefill): no host launches in the timing
+setattr(eng, a.knob, True)
+g = torch.cuda.CUDAGraph()
+run.prefill_run()
+torch.cuda.synchronize()
+with torch.cuda.graph(g):
+    run.prefill_run()
+torch.cuda.synchronize()
+for rnd in range(3):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(a.reps):
+        g.replay()
+    ev[1].record()
+    torch.cuda.synchronize()
+    gpu = ev[0].elapsed_time(ev[1]) / a.reps
+    res.setdefault("graph", []).append(round(gpu, 3))
+    print(f"graph prefill {gpu:.3f} ms", flush=True)
 print(json.dumps(res))
