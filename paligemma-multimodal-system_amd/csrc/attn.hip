@@ -35,7 +35,8 @@
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
 #ifndef PG_FA_SMALL
-#define PG_FA_SMALL 1     // prefill grids that leave most CUs idle at 4 waves (batch 1): 1- or 2-wave workgroups
+#define PG_FA_SMALL 0     // 1 = batch-1 prefill grids in 1- / 2-wave workgroups: measured slower (pt-224 prefill 5.69 vs
+                          // 5.47 ms: a lone wave's staging latency is exposed; Gemma 33.0 vs 22.7 us, SigLIP 13.6 vs 10.0)
 #endif
 
 // Decode (split mode): one wave per (batch, kv head, split); grid (1, Hkv * nsplit, B).

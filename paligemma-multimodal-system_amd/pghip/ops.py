@@ -303,9 +303,13 @@ def finalize_split(M: int, N: int, K: int) -> int:
     if math.ceil(M / 256) * math.ceil(N / 256) >= CUS:
         return 1
     tiles = math.ceil(M / 64) * math.ceil(N / 128)
-    if tiles >= 192:
+    # measured per call, graph-replayed with the finalisation included (scripts/tune/small_gemm_sweep.py,
+    # profiles/r03_small_gemm_sweep.txt): SigLIP q|k|v (108 tiles) 13.6 us unsplit vs 19.2 at split 3, fc1 (136)
+    # 14.9 vs 21.9 at split 2 -- the finalisation launch and the fp32 slabs cost more than the idle CUs; Gemma
+    # q|k|v (100 tiles) 17.2 at split 2 vs 20.9 unsplit / 21.7 at split 3
+    if tiles > 100:
         return 1
-    s = min(4, math.ceil(CUS / tiles), (K // 64) // 6)
+    s = min(2, math.ceil(CUS / tiles), (K // 64) // 6)
     return s if s >= 2 else 1
 
 
@@ -352,4 +356,6 @@ def gemm_ksplit(M: int, N: int, K: int) -> int:
     s256 = math.ceil(CUS / t256)
     if s256 <= min(16, (K // 64) // 8):
         return s256
-    return split_for(math.ceil(M / 64) * math.ceil(N / 128), K // 64)
+    # up to 6 splits: SigLIP o / fc2 at batch 1 (36 tiles) 6.1 / 11.4 us at split 6 vs 6.8 / 13.6 at 4, slower again
+    # at 9 (profiles/r03_small_gemm_sweep.txt)
+    return split_for(math.ceil(M / 64) * math.ceil(N / 128), K // 64, max_split=6)
