@@ -615,7 +615,7 @@ def test_gemm256_large_m(M, N, K):
         assert err(h, want) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K", [(264, 2560, 2048), (256, 3456, 1152), (256, 640, 1152)])
+@pytest.mark.parametrize("M,N,K", [(264, 2560, 2048), (256, 1536, 1152), (256, 640, 1152)])
 def test_split_k_finalize_epilogues(M, N, K):
     """Small-M bf16-epilogue GEMMs split K into fp32 slabs + pg_gemm_finalize: same outputs as the one-launch
     fused epilogue (bf16, gelu, gelu*up, V^T side output), up to fp32 summation order."""
