@@ -102,6 +102,9 @@ typedef struct PgFusedArgs {
  * spends a second row tile -- and a second weight read -- on the last M - 256 rows).  Measured on the
  * pt-224 Gemma gate/up (ks 1), down (ks 16) and o (ks 8) shapes. */
 #define PG_TILE_M1 0x400
+/* PG_TILE_N64 (tile GEMMs, M > 16, bf16 or fp8): 64 x 64 output tiles instead of 64 x 128 (or larger), twice
+ * the workgroups without a K split, for small-M GEMMs whose 64 x 128 grid leaves CUs idle. */
+#define PG_TILE_N64 0x800
 
 /* C = A[M][K] . W[N][K]^T with fused epilogue.  nn.Linear call sites: siglip.py:59-62,71-75,156,177-178,
  * 183-185; paligemma.py:57,64; gemma.py:205-207,212-218,255-259,274-278,356,484,523.  K % 32 == 0

@@ -98,6 +98,7 @@ __device__ __forceinline__ f32x4 load4_guard(const float* __restrict__ p, int n0
 
 #define PG_W_FRAG 0x100   // weight layout flag OR-ed into epi (include/pghip.h)
 #define PG_TILE_M1 0x400  // one row tile of all M (256..288) rows (include/pghip.h)
+#define PG_TILE_N64 0x800 // 64 x 64 tiles (include/pghip.h)
 #define PG_FP8 0x200      // A and W fp8 e4m3 with row scales (PgFusedArgs a_scale / w_scale), M > 16
 
 struct EpiArgs {
@@ -276,12 +277,14 @@ __device__ __forceinline__ size_t frag_off(int row, int k0, int c, int K) {
   return (size_t)(row >> 4) * 16 * K + ((size_t)(k0 >> 6) * 2 + (c & 1)) * 512 + ((c >> 1) * 16 + (row & 15)) * 8;
 }
 
-// Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread over the 4 waves.  FRAG: src is fragment-packed
-// (ld = K); each piece still reads 8 runs of 128 contiguous bytes.
-template <int ROWS, bool FRAG = false>
+// Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread evenly over NW staging waves (wave < NW; others issue none).
+// FRAG: src is fragment-packed (ld = K); each piece still reads 8 runs of 128 contiguous bytes.
+template <int ROWS, bool FRAG = false, int NW = 4>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int rows_valid,
                                            int k0, char* lds_tile, int wave, int lane) {
-  constexpr int PER_WAVE = ROWS / 32;
+  static_assert((ROWS / 8) % NW == 0, "pieces must split evenly over the staging waves");
+  constexpr int PER_WAVE = ROWS / 8 / NW;
+  if (wave >= NW) return;
 #pragma unroll
   for (int it = 0; it < PER_WAVE; ++it) {
     const int blk = wave * PER_WAVE + it;          // 1 KiB piece = 8 rows x 128 B
@@ -302,7 +305,13 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk)
 __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [0, 24]
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
@@ -313,22 +322,34 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
   }
 }
 
-template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false>
-__global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
-                                                        const bf16_t* __restrict__ W, int ldw, int K, int kchunk,
-                                                        int tiles_m, int tiles_n, EpiArgs e) {
+// WAVES (4, 8 or 12): waves per workgroup.  4: BM 64 as 1 x 4 waves of 64 x 32, BM 128 / 256 / 288 as 2 x 2.  More
+// waves put 2-3 waves on every SIMD, so one wave's LDS fragment reads hide behind another's MFMAs (with 4 waves the
+// single wave of a SIMD waits out every ds_read before its MFMAs): 8 = BM 64 as 2 x 4 waves of 32 x 32 and BM 256
+// as 4 x 2 of 64 x 64; 12 = BM 288 as 6 x 2 waves of 48 x 64.  The A pieces of a stage spread over all waves, the
+// W pieces over the first 8 (12 waves) so every wave's piece count -- its vmcnt step -- is a whole number.
+// BN = 64 (PG_TILE_N64, BM 64 and 4 waves only: 2 x 2 waves of 32 x 32): twice the workgroups of the 64 x 128
+// grid for the small-M prefill GEMMs whose 64 x 128 grid leaves most CUs idle, without a K split.
+template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN>
+__global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
+                                                               const bf16_t* __restrict__ W, int ldw, int K,
+                                                               int kchunk, int tiles_m, int tiles_n, EpiArgs e) {
   constexpr int A_BYTES = BM * TBK * 2;
-  constexpr int W_BYTES = TBN * TBK * 2;
+  static_assert(BN == TBN || (BN == 64 && BM == 64 && WAVES == 4), "BN 64: 64-row tiles of 4 waves only");
+  constexpr int W_BYTES = BN * TBK * 2;
   constexpr int STAGE_BYTES = A_BYTES + W_BYTES;
-  constexpr int P = BM / 32 + TBN / 32;            // glds pieces per wave per stage
-  constexpr int WN = BM == 64 ? 4 : 2;             // waves along N (BM 256 / 288: 2 x 2 waves of 128 / 144 rows)
-  constexpr int WM = 4 / WN;                       // waves along M
+  constexpr int WN = BN == 64 ? 2 : (WAVES == 4 ? (BM == 64 ? 4 : 2) : (WAVES == 8 ? (BM == 64 ? 4 : 2) : 2));
+  constexpr int WM = WAVES / WN;                   // waves along M
   constexpr int NI = BM / WM / 16;                 // 16-row subtiles per wave
-  constexpr int NJ = TBN / WN / 16;                // 16-col subtiles per wave
+  constexpr int NJ = BN / WN / 16;                 // 16-col subtiles per wave
+  static_assert(WM * NI * 16 == BM && WN * NJ * 16 == BN, "wave grid must tile the block");
+  constexpr int NWA = WAVES;                       // waves staging A pieces
+  constexpr int NWW = WAVES > 8 ? 8 : WAVES;       // waves staging W pieces
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  // glds pieces this wave issues per stage (wave-uniform): its vmcnt step per younger stage in flight
+  const int P = BM / 8 / NWA + (wave < NWW ? BN / 8 / NWW : 0);
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped tile order.
   const int nwg = gridDim.x;
@@ -343,7 +364,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
   const int gsize = min(tiles_m - first_m, GROUP);
   const int tm = first_m + (pid % gsize);
   const int tn = (pid % (GROUP * tiles_n)) / gsize;
-  const int m0 = tm * BM, n0 = tn * TBN;
+  const int m0 = tm * BM, n0 = tn * BN;
 
   const int z = blockIdx.z;
   const int kbeg = z * kchunk;
@@ -358,8 +379,8 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE_BYTES;
-    stage_tile<BM>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
-    stage_tile<TBN, FRAG>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
+    stage_tile<BM, false, NWA>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
+    stage_tile<BN, FRAG, NWW>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
   };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -382,7 +403,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int i = 0; i < NI; ++i) fa[i][s] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) fw[j][s] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
+        for (int j = 0; j < NJ; ++j) fw[j][s] = lds_frag(tW, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
       }
 #pragma unroll
       for (int i = 0; i < NI; ++i)
@@ -396,7 +417,7 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int i = 0; i < NI; ++i) fa[i] = lds_frag(tA, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) fw[j] = lds_frag(tW, wn * (TBN / WN) + j * 16 + (lane & 15), chunk);
+        for (int j = 0; j < NJ; ++j) fw[j] = lds_frag(tW, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -405,12 +426,12 @@ __global__ __launch_bounds__(256) void gemm_tile_kernel(const bf16_t* __restrict
     }
   }
 
-  // epilogue: acc[i][j] lane holds C[m = m0+wm*(BM/WM)+i*16+(lane&15)][n = n0+wn*(128/WN)+j*16+4*(lane>>4) + 0..3]
+  // epilogue: acc[i][j] lane holds C[m = m0+wm*(BM/WM)+i*16+(lane&15)][n = n0+wn*(BN/WN)+j*16+4*(lane>>4) + 0..3]
   const int q = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    const int nb = n0 + wn * (TBN / WN);
+    const int nb = n0 + wn * (BN / WN);
     if constexpr (F8) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) scale_acc(e, m, nb + j * 16 + q, acc[i][j]);
@@ -1313,9 +1334,31 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // has >= 256 workgroups; otherwise 64-row tiles with a 4-stage ring.  Split-K (fp32 partial epilogue
 // only) is chosen by the caller.
 // F8: A, W fp8 viewed as bf16-sized pairs (K, lda, ldw in 2-byte units: a 64-unit k-tile = 128 fp8 k)
+// waves per workgroup of each gemm_tile_kernel shape (4, or 8 / 12 -- see the kernel).  8 / 8 / 8 / 12 measured
+// 3-12 % faster than 4 on every batch-1 prefill GEMM and pt-224 prefill 5.29 -> 4.95 ms
+// (profiles/r03_tile_waves_ab.txt)
+#ifndef PG_TILE_W64
+#define PG_TILE_W64 8
+#endif
+#ifndef PG_TILE_W128
+#define PG_TILE_W128 8
+#endif
+#ifndef PG_TILE_W256
+#define PG_TILE_W256 8
+#endif
+#ifndef PG_TILE_W288
+#define PG_TILE_W288 12
+#endif
 template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
-                        hipStream_t st, bool m1 = false) {
+                        hipStream_t st, bool m1 = false, bool n64 = false) {
+  if (n64) {
+    const int m64 = (e.M + 63) / 64, tn = (e.N + 63) / 64;
+    const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st, A,
+                       lda, W, ldw, K, kchunk, m64, tn, e);
+    return;
+  }
   if constexpr (!F8) {
     if (m1) {
       // PG_TILE_M1 (batch-1 prefill: 256 image + a few text rows): ALL rows in one tile, so every weight tile
@@ -1323,10 +1366,12 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
       const int tiles_n = (e.N + TBN - 1) / TBN;
       const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
       if (e.M <= 256)
-        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 256, 3, FRAG>), dim3(tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 256, 3, FRAG, false, PG_TILE_W256>), dim3(tiles_n, 1, ksplit),
+                           dim3(64 * PG_TILE_W256), 0, st, A, lda,
                            W, ldw, K, kchunk, 1, tiles_n, e);
       else
-        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 288, 3, FRAG>), dim3(tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 288, 3, FRAG, false, PG_TILE_W288>), dim3(tiles_n, 1, ksplit),
+                           dim3(64 * PG_TILE_W288), 0, st, A, lda,
                            W, ldw, K, kchunk, 1, tiles_n, e);
       return;
     }
@@ -1343,13 +1388,15 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   const int t128 = ((e.M + 127) / 128) * tiles_n;
   if (t128 >= 256) {
     const int tiles_m = (e.M + 127) / 128;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG, F8>), dim3(tiles_m * tiles_n, 1, ksplit), dim3(256), 0, st,
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG, F8, PG_TILE_W128>), dim3(tiles_m * tiles_n, 1, ksplit),
+                       dim3(64 * PG_TILE_W128), 0, st,
                        A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
     return;
   }
   // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
   const int m64 = (e.M + 63) / 64;
-  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8>), dim3(m64 * tiles_n, 1, ksplit), dim3(256), 0, st, A, lda,
+  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),
+                     dim3(64 * PG_TILE_W64), 0, st, A, lda,
                      W, ldw, K, kchunk, m64, tiles_n, e);
 }
 
@@ -1414,11 +1461,11 @@ static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
 // M <= 16 -> weight-streaming GEMV, else the tile GEMM; FRAG (PG_W_FRAG) only for the Gemma epilogues
 template <int EPI, bool FRAG>
 static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
-                       hipStream_t st, bool m1 = false) {
+                       hipStream_t st, bool m1 = false, bool n64 = false) {
   if (e.M <= 16)
     launch_gemv<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
   else if constexpr (EPI != PG_EPI_F32_FIN)
-    launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st, m1);
+    launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st, m1, n64);
 }
 
 static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float* bias, void* C, int ldc,
@@ -1427,9 +1474,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   const bool frag = (epi_flags & PG_W_FRAG) != 0;
   const bool fp8 = (epi_flags & PG_FP8) != 0;
   const bool m1 = (epi_flags & PG_TILE_M1) != 0;
+  const bool n64 = (epi_flags & PG_TILE_N64) != 0;
   const int epi = epi_flags & 0xFF;
-  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8 | PG_TILE_M1)) == 0);
-  if (m1) PG_REQUIRE(!fp8 && M >= 256 && M <= 288 && (fa == nullptr || fa->pro_mode == 0));
+  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8 | PG_TILE_M1 | PG_TILE_N64)) == 0);
+  if (m1) PG_REQUIRE(!fp8 && !n64 && M >= 256 && M <= 288 && (fa == nullptr || fa->pro_mode == 0));
+  if (n64) PG_REQUIRE(M > 16);
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
@@ -1469,12 +1518,14 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
     PG_REQUIRE(!frag && M > 16 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && lda % 16 == 0 &&
                ldw % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0);
     switch (epi) {
-      case PG_EPI_BF16: launch_tile<PG_EPI_BF16, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+      case PG_EPI_BF16: launch_tile<PG_EPI_BF16, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream, false, n64); break;
       case PG_EPI_BF16_GELU_MUL:
-        launch_tile<PG_EPI_BF16_GELU_MUL, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
-      case PG_EPI_F32: launch_tile<PG_EPI_F32, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+        launch_tile<PG_EPI_BF16_GELU_MUL, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream, false, n64);
+        break;
+      case PG_EPI_F32: launch_tile<PG_EPI_F32, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream, false, n64); break;
       case PG_EPI_QKV_ROPE:
-        launch_tile<PG_EPI_QKV_ROPE, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream); break;
+        launch_tile<PG_EPI_QKV_ROPE, false, true>(a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream, false, n64);
+        break;
       default: return (int)hipErrorInvalidValue;
     }
     PG_LAUNCH_CHECK();
@@ -1482,11 +1533,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   }
 #define PG_CASE(E)                                                                             \
   case E:                                                                                      \
-    if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream, m1);                   \
-    else launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1);                       \
+    if (frag) launch_any<E, true>(a, lda, w, ldw, K, ksplit, e, stream, m1, n64);              \
+    else launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1, n64);                  \
     break;
 #define PG_CASE_ROWMAJOR(E)                                                                    \
-  case E: launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1); break;
+  case E: launch_any<E, false>(a, lda, w, ldw, K, ksplit, e, stream, m1, n64); break;
   switch (epi) {
     PG_CASE(PG_EPI_BF16)
     PG_CASE(PG_EPI_BF16_GELU_MUL)

