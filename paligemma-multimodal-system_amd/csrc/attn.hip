@@ -34,6 +34,9 @@
 #ifndef PG_ATTN_SPLIT_WAVES
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
+#ifndef PG_FA_DEEP
+#define PG_FA_DEEP 1      // 4-wave prefill workgroups (grids short of the chip, batch 1): the 5-8 stage ring
+#endif
 #ifndef PG_FA_SMALL
 #define PG_FA_SMALL 0     // 1 = batch-1 prefill grids in 1- / 2-wave workgroups: measured slower (pt-224 prefill 5.69 vs
                           // 5.47 ms: a lone wave's staging latency is exposed; Gemma 33.0 vs 22.7 us, SigLIP 13.6 vs 10.0)
@@ -422,26 +425,31 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
 }
 
 // Prefill flash attention, LDS-DMA staged (no mask, 16-B aligned strides).  A workgroup of WAVES waves
-// (16 query rows each) walks 64-key blocks; every block's K [64 keys][DP] and V^T [DT*16 d][64 keys] are
-// pulled HBM->LDS by global_load_lds (16 B/lane, lane-linear destinations) into a 2-stage ring, the next
-// block in flight while the current one is computed.  Images:
+// (16 query rows each) walks KB-key blocks (KB 64 or 32); every block's K [KB keys][DP] and V^T [DT*16 d][KB keys]
+// are pulled HBM->LDS by global_load_lds (16 B/lane, lane-linear destinations) into an NST-stage ring: NST - 1
+// blocks in flight while one is computed, the wait for a block a counted vmcnt (its younger blocks stay in flight
+// across the barrier).  NST 2 / KB 64 for grids that fill the chip; a deep ring (NST 5-8) for the batch-1 grids
+// of a few dozen workgroups, whose time is otherwise one L2 round trip per block.  Images:
 //   K   : 16-key groups of [DP/8 chunks][16 keys][16 B] -> a S^T fragment read (16 keys x 32 d) is one
 //         contiguous KiB per wave-instruction (conflict-free ds_read_b128)
-//   V^T : rows of 128 B (64 keys), 16-B chunk XOR-swizzled by (row >> 1) & 7 through the source address
-//         -> the two ds_read_b64 of a PV fragment are conflict-free
+//   V^T : rows of 2 KB bytes, 16-B chunk XOR-swizzled through the source address by (row >> 1) & 7 (KB 64) or
+//         (row >> 2) & 3 (KB 32) -> the two ds_read_b64 of a PV fragment are conflict-free
 // Per block a wave does 4 x KS S^T MFMAs, an online softmax on 16 scores per lane (the rescale of O is
 // skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
 // V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row);
 // K dims past D (D < DP) are never read from memory.
-template <int DP, int DT, int WAVES, int RPW>
+template <int DP, int DT, int WAVES, int RPW, int KB = 64, int NST = 2>
 __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
+  static_assert(KB == 64 || KB == 32, "64- or 32-key blocks");
   constexpr int KS = DP / 32;
   constexpr int NCH = DP / 8;                      // 16-B chunks per K row
-  constexpr int KIMG = 64 * DP * 2;                // bytes
-  constexpr int VIMG = DT * 16 * 128;
+  constexpr int KIMG = KB * DP * 2;                // bytes
+  constexpr int VROW = KB * 2;                     // bytes per V^T image row
+  constexpr int VIMG = DT * 16 * VROW;
   constexpr int STAGE = KIMG + VIMG;
   constexpr int KINS = KIMG / 1024, VINS = VIMG / 1024;   // glds wave-instructions per block
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  static_assert(KIMG % 1024 == 0 && VIMG % 1024 == 0 && NST * STAGE <= 163840, "stage images");
+  __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
   const int t = threadIdx.x;
   const int lane = t & 63, wave = t >> 6, c = lane & 15, g = lane >> 4;
@@ -482,12 +490,14 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(kimg + i * 1024), 16, 0, 0);
     }
     for (int i = wave; i < VINS; i += WAVES) {
-      const int row = 8 * i + (lane >> 3);
-      const int cl = (lane & 7) ^ ((row >> 1) & 7);
+      const int row = KB == 64 ? 8 * i + (lane >> 3) : 16 * i + (lane >> 2);
+      const int cl = KB == 64 ? (lane & 7) ^ ((row >> 1) & 7) : (lane & 3) ^ ((row >> 2) & 3);
       const bf16_t* src = vbase + (long)min(row, D - 1) * a.vt_ds + min(kb + 8 * cl, vkey_max);
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(vimg + i * 1024), 16, 0, 0);
     }
   };
+  // glds pieces this wave issues per block (wave-uniform): its vmcnt step per younger block in flight
+  const int P = (KINS > wave ? (KINS - 1 - wave) / WAVES + 1 : 0) + (VINS > wave ? (VINS - 1 - wave) / WAVES + 1 : 0);
 
   f32x4 o[RPW][DT];
   float m[RPW], l[RPW];
@@ -498,56 +508,60 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
     for (int tt = 0; tt < DT; ++tt) o[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int nblk = (Lkv + 63) / 64;
+  const int nblk = (Lkv + KB - 1) / KB;
+  constexpr int NKT = KB / 16;                     // 16-key groups per block
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int sb = 0; sb < NST - 1; ++sb)
+    if (sb < nblk) stage(sb * KB, sb);
   for (int ib = 0; ib < nblk; ++ib) {
-    const int kb = ib * 64;
-    if (ib + 1 < nblk) stage(kb + 64, (ib + 1) & 1);   // that buffer was last read before the previous barrier
-    const char* kimg = smem + (ib & 1) * STAGE;
+    const int kb = ib * KB;
+    // block ib has landed once at most (blocks issued after it) * P of this wave's pieces are outstanding
+    wait_vm_n((min(nblk - 1, ib + NST - 2) - ib) * P);
+    __builtin_amdgcn_s_barrier();                  // every wave's pieces of ib landed; block ib - 1 fully read
+    if (ib + NST - 1 < nblk) stage(kb + (NST - 1) * KB, (ib + NST - 1) % NST);   // the buffer block ib - 1 used
+    const char* kimg = smem + (ib % NST) * STAGE;
     const char* vimg = kimg + KIMG;
-    // ---- S^T for 4 groups of 16 keys
-    f32x4 sc[RPW][4];
+    // ---- S^T for NKT groups of 16 keys
+    f32x4 sc[RPW][NKT];
 #pragma unroll
     for (int i = 0; i < RPW; ++i)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) sc[i][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kt = 0; kt < NKT; ++kt) sc[i][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
+      for (int kt = 0; kt < NKT; ++kt) {
         const bf16x8 kf = *(const bf16x8*)(kimg + ((kt * NCH + 4 * s + g) * 16 + c) * 16);
 #pragma unroll
         for (int i = 0; i < RPW; ++i) sc[i][kt] = mfma16(kf, qf[i][s], sc[i][kt]);
       }
     // lane holds S[key = kb + 16 kt + 4g + j][q = c] of each row group
-    bf16x8 pf[RPW][2];
+    bf16x8 pf[RPW][KB / 32];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
-      float x[16];
+      float x[4 * NKT];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[i][kt][j] * a.scale_log2;
-      if (kb + 64 > Lkv) {
+      if (kb + KB > Lkv) {
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (kb + 16 * kt + 4 * g + j >= Lkv) x[4 * kt + j] = -INFINITY;
       }
       float bm = x[0];
 #pragma unroll
-      for (int j = 1; j < 16; ++j) bm = fmaxf(bm, x[j]);
+      for (int j = 1; j < 4 * NKT; ++j) bm = fmaxf(bm, x[j]);
       bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
       bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
       const float mn = fmaxf(m[i], bm);
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
       float rs = 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
+      for (int j = 0; j < 4 * NKT; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       l[i] = l[i] * alpha + rs;
@@ -558,7 +572,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       }
       // P^T operand of the two 32-key steps; slot 8g+j <-> key 32h + 4g + j (j < 4), 32h + 16 + 4g + j - 4
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < KB / 32; ++h) {
         u32x4 pw;
         pw[0] = pack_bf2(x[8 * h + 0], x[8 * h + 1]);
         pw[1] = pack_bf2(x[8 * h + 2], x[8 * h + 3]);
@@ -569,12 +583,12 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     }
     // ---- O^T += V^T . P^T: one V^T fragment read feeds the RPW row groups
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < KB / 32; ++h) {
 #pragma unroll
       for (int tt = 0; tt < DT; ++tt) {
         const int row = 16 * tt + c;
-        const char* vr = vimg + row * 128;
-        const int sw = (row >> 1) & 7;
+        const char* vr = vimg + row * VROW;
+        const int sw = KB == 64 ? (row >> 1) & 7 : (row >> 2) & 3;
         const int c0 = 4 * h, c1 = 4 * h + 2;                 // 16-B chunks of keys 32h + 4g.. and 32h + 16 + 4g..
         const u32x2 v0 = *(const u32x2*)(vr + ((c0 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
         const u32x2 v1 = *(const u32x2*)(vr + ((c1 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
@@ -583,8 +597,6 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
         for (int i = 0; i < RPW; ++i) o[i][tt] = mfma16(vf, pf[i][h], o[i][tt]);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // next block landed (this wave's loads)
-    __builtin_amdgcn_s_barrier();                        // ... every wave's; this buffer fully read
   }
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
@@ -679,8 +691,22 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 #define PG_FA_RPW 1
 #endif
 
+// the deep ring of a 4-wave workgroup: 64-key blocks when >= 4 stages fit the 160 KiB of LDS, else 32-key blocks
 template <int DP, int DT>
-static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const AttnArgs& a) {
+struct FaDeep {
+  static constexpr int S64 = 64 * DP * 2 + DT * 16 * 128, S32 = 32 * DP * 2 + DT * 16 * 64;
+  static constexpr int KB = 163840 / S64 >= 4 ? 64 : 32;
+  static constexpr int N = 163840 / (KB == 64 ? S64 : S32);
+  static constexpr int NST = N > 8 ? 8 : N;
+};
+
+template <int DP, int DT>
+static void launch_fa(int waves, int rpw, bool deep, dim3 grid, hipStream_t stream, const AttnArgs& a) {
+  if (deep && waves == 4 && rpw == 1) {
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 4, 1, FaDeep<DP, DT>::KB, FaDeep<DP, DT>::NST>), grid, dim3(256), 0,
+                       stream, a);
+    return;
+  }
   if constexpr (PG_FA_RPW == 2) {
     if constexpr (DP <= 96) {       // (DP 128 at 8 x 32 rows needs > 256 registers: 1 wave / SIMD)
       if (waves == 8 && rpw == 2) {
@@ -713,7 +739,7 @@ static void launch_fa(int waves, int rpw, dim3 grid, hipStream_t stream, const A
 #define ATTN_DISPATCH(DP_, DT_)                                                             \
   if (DP == DP_ && DT == DT_) {                                                              \
     if (fa_waves)                                                                            \
-      launch_fa<DP_, DT_>(fa_waves, fa_rpw, grid, stream, a);                                \
+      launch_fa<DP_, DT_>(fa_waves, fa_rpw, fa_deep, grid, stream, a);                       \
     else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
     else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32 && PG_ATTN_WG && DP_ == 256 && \
@@ -765,6 +791,7 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
                        ((uintptr_t)vt & 15) == 0;
   // LDS-DMA flash kernel for every unmasked prefill; 8 waves (128 rows) per workgroup once that fills the chip
   int fa_waves = 0, fa_rpw = 1;
+  bool fa_deep = false;
   if (split_keys == 0 && mask == nullptr && aligned && lkv_dev == nullptr && PG_ATTN_FA) {
     auto wgs = [&](int rows) { return (long)((Lq * G + rows - 1) / rows) * Hkv * B; };
     // two 16-row groups per wave (half the LDS fragment reads per flop) when the grid still fills the chip:
@@ -787,6 +814,7 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
     }
     const int rows = 16 * fa_waves * fa_rpw;
     grid = dim3((Lq * G + rows - 1) / rows, Hkv, B);
+    fa_deep = PG_FA_DEEP && fa_waves == 4 && fa_rpw == 1;
   }
   const bool use_lds = fa_waves == 0 && split_keys == 0 && wgs16 >= 1024 && aligned;
   if (fa_waves) {

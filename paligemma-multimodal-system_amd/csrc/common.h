@@ -84,5 +84,18 @@ __device__ __forceinline__ float block_sum(float v, float* red /* >= 16 floats o
 static __device__ int pg_zero_word = 0;
 
 // error reporting: every C entry point returns a hipError_t as int (0 = ok)
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the counter field takes an immediate); n > 40 waits for all
+#define PG_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    PG_VMC(1) PG_VMC(2) PG_VMC(3) PG_VMC(4) PG_VMC(5) PG_VMC(6) PG_VMC(7) PG_VMC(8) PG_VMC(9) PG_VMC(10)
+    PG_VMC(11) PG_VMC(12) PG_VMC(13) PG_VMC(14) PG_VMC(15) PG_VMC(16) PG_VMC(17) PG_VMC(18) PG_VMC(19) PG_VMC(20)
+    PG_VMC(21) PG_VMC(22) PG_VMC(23) PG_VMC(24) PG_VMC(25) PG_VMC(26) PG_VMC(27) PG_VMC(28) PG_VMC(29) PG_VMC(30)
+    PG_VMC(31) PG_VMC(32) PG_VMC(33) PG_VMC(34) PG_VMC(35) PG_VMC(36) PG_VMC(37) PG_VMC(38) PG_VMC(39) PG_VMC(40)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+#undef PG_VMC
+
 #define PG_LAUNCH_CHECK() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
 #define PG_REQUIRE(cond) do { if (!(cond)) return (int)hipErrorInvalidValue; } while (0)

@@ -322,6 +322,9 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
   }
 }
 
+#ifndef PG_TILE_PROBE
+#define PG_TILE_PROBE 0   // tuning builds only: 1 = staging without MFMAs, 2 = MFMAs without staging (wrong results)
+#endif
 // WAVES (4, 8 or 12): waves per workgroup.  4: BM 64 as 1 x 4 waves of 64 x 32, BM 128 / 256 / 288 as 2 x 2.  More
 // waves put 2-3 waves on every SIMD, so one wave's LDS fragment reads hide behind another's MFMAs (with 4 waves the
 // single wave of a SIMD waits out every ds_read before its MFMAs): 8 = BM 64 as 2 x 4 waves of 32 x 32 and BM 256
@@ -379,6 +382,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE_BYTES;
+    if (PG_TILE_PROBE == 2) return;                // tuning probe: no loads (MFMA + barrier floor)
     stage_tile<BM, false, NWA>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
     stage_tile<BN, FRAG, NWW>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
   };
@@ -389,12 +393,15 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt has landed once at most (issued stages after kt) * P pieces are outstanding
     const int younger = min(nk - 1, kt + STAGES - 2) - kt;
-    wait_vm(younger * P);
+    wait_vm_n(younger * P);
     __builtin_amdgcn_s_barrier();                  // every wave's pieces of kt landed; kt-1 fully read
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
     const char* tA = smem + (kt % STAGES) * STAGE_BYTES;
     const char* tW = tA + A_BYTES;
-    if constexpr (F8) {
+    if constexpr (PG_TILE_PROBE == 1) {
+      // tuning probe: no fragment reads or MFMAs (the staging pipeline's floor); one LDS word keeps the loads live
+      if (lane == 0 && wave == 0) acc[0][0][0] += *(const float*)tA;
+    } else if constexpr (F8) {
       // fp8: the 128-byte k-row holds 128 k; one 16x16x128 MFMA takes both chunk sets of the bf16 form
       bf16x8 fa[NI][2], fw[NJ][2];
 #pragma unroll
@@ -567,8 +574,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   };
 
   // prologue: all of tile 0, then the three halves of tile 1 that phases 1-3 of tile -1 would have issued
+  // (a split past the end of K -- ksplit with ceil-sized slices -- stages nothing and stores a zero slab)
+  if (nk > 0) {
 #pragma unroll
-  for (int h = 0; h < 4; ++h) stage(h, 0);
+    for (int h = 0; h < 4; ++h) stage(h, 0);
+  }
   if (nk > 1) {
     stage(0, 1);
     stage(3, 1);
@@ -1337,6 +1347,9 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // waves per workgroup of each gemm_tile_kernel shape (4, or 8 / 12 -- see the kernel).  8 / 8 / 8 / 12 measured
 // 3-12 % faster than 4 on every batch-1 prefill GEMM and pt-224 prefill 5.29 -> 4.95 ms
 // (profiles/r03_tile_waves_ab.txt)
+#ifndef PG_TILE_DEEP
+#define PG_TILE_DEEP 0    // 64-row tiles in a one-round grid: deeper staging rings (tuning)
+#endif
 #ifndef PG_TILE_W64
 #define PG_TILE_W64 8
 #endif
@@ -1355,8 +1368,13 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   if (n64) {
     const int m64 = (e.M + 63) / 64, tn = (e.N + 63) / 64;
     const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st, A,
-                       lda, W, ldw, K, kchunk, m64, tn, e);
+    // a grid of one round: a 9-stage ring (144 KiB, 8 k-tiles in flight) instead of 4 (64 KiB, 2 workgroups / CU)
+    if (PG_TILE_DEEP && m64 * tn * ksplit <= 256)
+      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 9, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
+                         A, lda, W, ldw, K, kchunk, m64, tn, e);
+    else
+      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
+                         A, lda, W, ldw, K, kchunk, m64, tn, e);
     return;
   }
   if constexpr (!F8) {
@@ -1395,6 +1413,11 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   }
   // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
   const int m64 = (e.M + 63) / 64;
+  if (PG_TILE_DEEP && m64 * tiles_n * ksplit <= 256) {   // one round: 6 stages (144 KiB) instead of 4 (96 KiB)
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 6, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),
+                       dim3(64 * PG_TILE_W64), 0, st, A, lda, W, ldw, K, kchunk, m64, tiles_n, e);
+    return;
+  }
   hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),
                      dim3(64 * PG_TILE_W64), 0, st, A, lda,
                      W, ldw, K, kchunk, m64, tiles_n, e);

@@ -25,6 +25,12 @@ SHAPES = [  # name, M, N, K, epi, copies
     ("gemma_down", 264, 2048, 16384, ops.EPI_F32, 18),
 ]
 TILES = ((0, "t64"), (ops.TILE_M1, "m1"), (ops.TILE_N64, "n64"))
+# SWEEP_SHAPES / SWEEP_TILES / SWEEP_KS (comma lists) restrict the sweep; SWEEP_BLAS=0 skips the library GEMM
+if os.environ.get("SWEEP_SHAPES"):
+    SHAPES = [x for x in SHAPES if x[0] in os.environ["SWEEP_SHAPES"].split(",")]
+if os.environ.get("SWEEP_TILES"):
+    TILES = tuple(x for x in TILES if x[1] in os.environ["SWEEP_TILES"].split(","))
+KS = tuple(int(k) for k in os.environ.get("SWEEP_KS", "1,2,3,4,6,9,12,18").split(","))
 
 
 def run(name, M, N, K, epi, copies, flags, ks):
@@ -82,10 +88,42 @@ def run(name, M, N, K, epi, copies, flags, ks):
     return ev[0].elapsed_time(ev[1]) * 1000 / (5 * copies), e
 
 
+def blas(M, N, K, copies):
+    """torch.matmul (hipBLASLt) on the same shape, plain bf16 output: the library GEMM as a yardstick."""
+    Ws = [torch.randn(N, K, device="cuda").div_(K ** 0.5).to(torch.bfloat16) for _ in range(copies)]
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    for W in Ws:
+        torch.matmul(A, W.t(), out=out)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for W in Ws:
+                torch.matmul(A, W.t(), out=out)
+    g.replay()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(5):
+        g.replay()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) * 1000 / (5 * copies)
+
+
 res = {"lib": os.path.basename(os.environ.get("PGHIP_LIB", "libpghip.so"))}
 for name, M, N, K, epi, copies in SHAPES:
+    try:
+        if os.environ.get("SWEEP_BLAS", "1") != "0":
+            us = blas(M, N, K, copies)
+            res[f"{name}/blas"] = round(us, 2)
+            print(f"{name:11s} blas     {us:8.2f} us  {2 * M * N * K / us / 1e6:7.1f} TF/s", flush=True)
+    except Exception as e:  # noqa: BLE001
+        print(f"{name:11s} blas failed: {str(e)[:80]}", flush=True)
     for flags, tag in TILES:
-        for ks in (1, 2, 3, 4, 6, 9, 12, 18):
+        for ks in KS:
             if (K // 64) // ks < 2:
                 continue
             us, e = run(name, M, N, K, epi, copies, flags, ks)

@@ -67,6 +67,20 @@ def test_gemm_split_k_partials(M):
         assert err(part.sum(0), A.float() @ W.float().t() + bias) < 1e-5
 
 
+@pytest.mark.parametrize("tile", ["g256", "t64", "n64"])
+def test_gemm_split_k_past_the_end_of_k(tile):
+    """A split whose ceil-sized k-slices run past K (32 k-tiles in 12 slices of 3: slice 11 is empty) stores a zero
+    slab and reads nothing past K, on the 256x256 kernel (264 x 32768: 256 tiles), the 64-row and the 64x64 tiles."""
+    from pghip import ops
+    M, N, K, s = (264, 32768, 2048, 12) if tile == "g256" else (100, 512, 2048, 12)
+    A, W = rnd(M, K, seed=51), rnd(N, K, scale=1 / 45, seed=52)
+    part = torch.full((s, M, N), float("nan"), dtype=torch.float32, device="cuda")
+    ops.gemm(A, W, part, epi=ops.EPI_F32 | (ops.TILE_N64 if tile == "n64" else 0), ksplit=s)
+    torch.cuda.synchronize()
+    assert (part[11] == 0).all()
+    assert err(part.sum(0), A.float() @ W.float().t()) < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K,s", [(300, 256, 512, 2), (16512, 2048, 2048, 1), (16512, 2048, 4096, 3)])
 def test_gemm_slab_rows_row_blocks(M, N, K, s):
     """PgFusedArgs.slab_rows: a split-K fp32 GEMM issued as a head of whole 256-row tiles plus a ragged tail,

@@ -89,5 +89,5 @@ def test_tp2_full_size_pt224(tmp_path, comm):
         assert o["decode_err_vs_solo"] < 2e-2, o
         assert o["decode_disagree"] == [], o
         assert o["greedy_tp"] == o["greedy_ref"], o
-        assert o["sampled_tp"][0] == o["sampled_first_want"], o
+        assert o["sampled_first_ok"], o
     assert res[0]["greedy_tp"] == res[1]["greedy_tp"] and res[0]["sampled_tp"] == res[1]["sampled_tp"]

@@ -20,6 +20,32 @@ def err(a, b):
     return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
 
 
+def topp_draw_ok(logits, got, T, P, u):
+    """The kernel's top-p draw `got` equals the oracle's explicit-uniform inverse-CDF draw (oracle.sample_top_p) from
+    logits [V], up to fp32 summation order: the kept set may differ by a token whose mass ranked before it lies
+    within 1e-5 of top_p (the reference's torch.cumsum vs the kernel's select), and the draw may fall on either side
+    of a CDF step within 1e-6 of the uniform's position."""
+    from oracle import paligemma_oracle as O
+    if got == int(O.sample_top_p(logits[None], T, P, np.array([u], np.float32))[0, 0]):
+        return True
+    x = logits.astype(np.float64) / T
+    p = np.exp(x - x.max())
+    p /= p.sum()
+    order = np.argsort(-p, kind="stable")
+    before = np.empty_like(p)
+    before[order] = np.cumsum(p[order]) - p[order]
+    kept = before <= P
+    variants = [kept] + [np.where(np.arange(p.size) == t, ~kept, kept) for t in np.nonzero(np.abs(before - P) < 1e-5)[0]]
+    for k in variants:
+        q = np.where(k, p, 0.0)
+        c = np.cumsum(q)
+        t = u * c[-1]
+        lo = c[got] - q[got]
+        if q[got] > 0 and lo - 1e-6 * c[-1] <= t <= c[got] + 1e-6 * c[-1]:
+            return True
+    return False
+
+
 def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -139,10 +165,10 @@ def full_size(rank, world, name):
         sb = np.sort(b)[::-1]
         if sb[0] - sb[1] > 0.05 and int(a.argmax()) != int(b.argmax()):
             disagree.append(t)
-        # the sampled id equals the oracle's explicit-uniform draw from the same (TP-gathered) logits
-        want = int(O.sample_top_p(a[None], 0.8, 0.9, np.array([0.5], np.float32))[0, 0])
-        if int(st[0]["ids"][0]) != want:
-            disagree.append(("topp", t, int(st[0]["ids"][0]), want))
+        # the sampled id is the oracle's explicit-uniform draw from the same (TP-gathered) logits
+        got = int(st[0]["ids"][0])
+        if not topp_draw_ok(a, got, 0.8, 0.9, 0.5):
+            disagree.append(("topp", t, got, int(O.sample_top_p(a[None], 0.8, 0.9, np.array([0.5], np.float32))[0, 0])))
     out["decode_err_vs_solo"] = worst
     out["decode_disagree"] = disagree
     # free-running greedy through the decode graph (when the communicator allows) vs the reference's 32 ids, and
@@ -155,8 +181,8 @@ def full_size(rank, world, name):
     # (free-running draws are not compared with the single-rank engine: the TP logits differ from it by ~1e-2 in
     # another fp32 summation order, and on this flat synthetic distribution that moves a uniform across a CDF
     # boundary within a few steps -- measured at step 1.  Each draw's parity is the teacher-forced check above.)
-    out["sampled_first_want"] = int(O.sample_top_p(res[0][2][:1].float().cpu().numpy(), 0.8, 0.9,
-                                                   u[0].numpy().astype(np.float32))[0, 0])
+    out["sampled_first_ok"] = topp_draw_ok(res[0][2][0].float().cpu().numpy(), out["sampled_tp"][0], 0.8, 0.9,
+                                           float(u[0, 0]))
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
     if isinstance(comm, XgmiComm):
