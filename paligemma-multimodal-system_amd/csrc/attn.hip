@@ -35,7 +35,8 @@
 #define PG_ATTN_SPLIT_WAVES 1
 #endif
 #ifndef PG_FA_DEEP
-#define PG_FA_DEEP 1      // 4-wave prefill workgroups (grids short of the chip, batch 1): the 5-8 stage ring
+#define PG_FA_DEEP 0      // 4-wave prefill workgroups: a 5-8 stage ring; measured slower (pt-224 Gemma 25.2 vs 22.7 us,
+                          // SigLIP 10.0 vs 10.0: not latency-bound; profiles/r03_prefill_breakdown_pt224.txt)
 #endif
 #ifndef PG_FA_SMALL
 #define PG_FA_SMALL 0     // 1 = batch-1 prefill grids in 1- / 2-wave workgroups: measured slower (pt-224 prefill 5.69 vs
@@ -50,19 +51,40 @@ __global__ __launch_bounds__(64) void attn_decode_kernel(AttnArgs a) {
                                          threadIdx.x);
 }
 
-// Decode (split mode) with NW-block splits (split_keys = 32 * NW): one workgroup of NW waves per (batch, kv head,
-// split), wave w takes the split's 32-key block w (all blocks' loads in flight at once, one memory round trip
-// instead of NW sequential ones), and the waves' (O, m, l) are merged through LDS into ONE partial of the split
-// (2^(m_w - M) weights, the merge of pg_attn_combine), so the combine still sees nsplit partials.  Needs a known
-// cache capacity (kcap >= 32) and head_dim == DP.  grid (1, Hkv * nsplit, B).
+// Decode (split mode) with NW * NB-block splits (split_keys = 32 * NW * NB): one workgroup of NW waves per (batch,
+// kv head, split); in round j < NB wave w takes the split's 32-key block j * NW + w (the NW waves' loads in flight
+// at once, one memory round trip per round), folding its rounds into one running (O, m, l); then the waves'
+// (O, m, l) are merged through LDS into ONE partial of the split (2^(m_w - M) weights, the merge of
+// pg_attn_combine), so the combine still sees nsplit partials.  NB > 1 sizes the grid to one round of resident
+// workgroups at long KV x batch (pt-896 x32: 12 splits of 384 keys, 384 workgroups, instead of 36 of 128 keys in
+// 2.25 rounds).  Rounds past the kv length are skipped.  Needs a known cache capacity (kcap >= 32) and
+// head_dim == DP.  grid (1, Hkv * nsplit, B).
 template <int DP, int DT, int NW>
 __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int nsplit = (int)gridDim.y / a.Hkv;
   const int b = blockIdx.z, kvh = blockIdx.y / nsplit, sp = blockIdx.y % nsplit;
+  const int NB = a.split_keys / (32 * NW);
   f32x4 o[DT];
   float m, l;
   attn_decode_block32<DP, DT>(a, b, kvh, sp * a.split_keys + 32 * wave, lane, o, m, l);
+  if (NB > 1) {
+    const int lkv = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(a.lkv_dev ? a.lkv_dev : &pg_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + a.Lkv;
+    for (int j = 1; j < NB; ++j) {
+      const int kb = sp * a.split_keys + (j * NW + wave) * 32;
+      if (kb >= lkv) break;                        // wave-uniform: no key of this or a later round is valid
+      f32x4 oj[DT];
+      float mj, lj;
+      attn_decode_block32<DP, DT>(a, b, kvh, kb, lane, oj, mj, lj);
+      const float mn = fmaxf(m, mj);
+      const float wa = m == -INFINITY ? 0.f : exp2f(m - mn), wb = mj == -INFINITY ? 0.f : exp2f(mj - mn);
+      l = l * wa + lj * wb;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[t] = o[t] * wa + oj[t] * wb;
+    }
+  }
   __shared__ f32x4 so[NW - 1][DT][64];
   __shared__ float sml[NW - 1][2][16];
   if (wave > 0) {
@@ -457,13 +479,17 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   const int Lkv = a.Lkv;
   const int R = a.Lq * a.G;
   const int D = a.D;
+  // key split (a.pf_splits > 1): workgroup x = row tile * nks + split; split ks walks its share of the key blocks
+  const int nks = a.pf_splits > 1 ? a.pf_splits : 1;
+  const int rt = blockIdx.x / nks, ks = blockIdx.x % nks;
   // RPW groups of 16 query rows per wave: every K / V^T fragment read from LDS feeds RPW MFMAs
-  int pos[RPW], hq[RPW];
+  int pos[RPW], hq[RPW], rrow[RPW];
   bool rvalid[RPW];
   bf16x8 qf[RPW][KS];
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
-    const int r = ((blockIdx.x * WAVES + wave) * RPW + i) * 16 + c;
+    const int r = ((rt * WAVES + wave) * RPW + i) * 16 + c;
+    rrow[i] = r;
     rvalid[i] = r < R;
     pos[i] = rvalid[i] ? r / a.G : 0;
     hq[i] = kvh * a.G + (rvalid[i] ? r % a.G : 0);
@@ -508,14 +534,17 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
     for (int tt = 0; tt < DT; ++tt) o[i][tt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int nblk = (Lkv + KB - 1) / KB;
+  const int nblk_all = (Lkv + KB - 1) / KB;
+  const int per = (nblk_all + nks - 1) / nks;
+  const int kb0 = ks * per * KB;                   // first key of this split
+  const int nblk = max(0, min(nblk_all - ks * per, per));
   constexpr int NKT = KB / 16;                     // 16-key groups per block
 
 #pragma unroll
   for (int sb = 0; sb < NST - 1; ++sb)
-    if (sb < nblk) stage(sb * KB, sb);
+    if (sb < nblk) stage(kb0 + sb * KB, sb);
   for (int ib = 0; ib < nblk; ++ib) {
-    const int kb = ib * KB;
+    const int kb = kb0 + ib * KB;
     // block ib has landed once at most (blocks issued after it) * P of this wave's pieces are outstanding
     wait_vm_n((min(nblk - 1, ib + NST - 2) - ib) * P);
     __builtin_amdgcn_s_barrier();                  // every wave's pieces of ib landed; block ib - 1 fully read
@@ -597,6 +626,19 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
         for (int i = 0; i < RPW; ++i) o[i][tt] = mfma16(vf, pf[i][h], o[i][tt]);
       }
     }
+  }
+  if (nks > 1) {
+    // unnormalised O and the row's (m, l) of this key split
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      if (!rvalid[i]) continue;
+      const long prow = (((long)b * a.Hkv + kvh) * nks + ks) * R + rrow[i];
+      float* po = a.part_o + prow * (DT * 16);
+#pragma unroll
+      for (int tt = 0; tt < DT; ++tt) *(f32x4*)(po + 16 * tt + 4 * g) = o[i][tt];
+      if (g == 0) *(f32x2*)(a.part_ml + prow * 2) = f32x2{m[i], l[i]};
+    }
+    return;
   }
 #pragma unroll
   for (int i = 0; i < RPW; ++i) {
@@ -685,6 +727,50 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
   }
 }
 
+// Merge the key-split prefill partials: o[b][pos][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s, one thread
+// per (row, 4 dims), every split's (m, l, O) loaded before the first is used.
+#define PF_MAXS 8
+__global__ __launch_bounds__(256) void attn_pf_combine_kernel(const float* __restrict__ part_o,
+                                                              const float* __restrict__ part_ml, int nks, int R, int G,
+                                                              int Hkv, int D, int DW, int Lq, bf16_t* __restrict__ o,
+                                                              long o_rs, long total) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int D4 = D >> 2;
+  const int d4 = (int)(idx % D4);
+  const long rowg = idx / D4;
+  const int r = (int)(rowg % R);
+  const long bk = rowg / R;                        // b * Hkv + kvh
+  f32x2 ml[PF_MAXS];
+  f32x4 ov[PF_MAXS];
+#pragma unroll
+  for (int s = 0; s < PF_MAXS; ++s) {
+    const long prow = (bk * nks + min(s, nks - 1)) * R + r;
+    ml[s] = *(const f32x2*)(part_ml + prow * 2);
+    ov[s] = *(const f32x4*)(part_o + prow * DW + 4 * d4);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float M = -INFINITY;
+#pragma unroll
+  for (int s = 0; s < PF_MAXS; ++s)
+    if (s < nks) M = fmaxf(M, ml[s][0]);
+  float den = 0.f;
+  f32x4 num = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < PF_MAXS; ++s) {
+    const float w = (s < nks && ml[s][0] != -INFINITY) ? exp2f(ml[s][0] - M) : 0.f;
+    den += w * ml[s][1];
+    num += w * ov[s];
+  }
+  const float inv = 1.0f / den;
+  const int b = (int)(bk / Hkv), kvh = (int)(bk % Hkv);
+  const int pos = r / G, hq = kvh * G + r % G;
+  u32x2 p;
+  p[0] = pack_bf2(num[0] * inv, num[1] * inv);
+  p[1] = pack_bf2(num[2] * inv, num[3] * inv);
+  *(u32x2*)(o + ((long)b * Lq + pos) * o_rs + (long)hq * D + 4 * d4) = p;
+}
+
 // Flash attention, 16-row query groups per wave.  2 (one K / V^T fragment read feeding two row groups,
 // 4 waves at head_dim 256) measured 0.81x at pt-448 Gemma, 0.95x / 1.03x at SigLIP 448 / 896: default 1.
 #ifndef PG_FA_RPW
@@ -743,13 +829,11 @@ static void launch_fa(int waves, int rpw, bool deep, dim3 grid, hipStream_t stre
     else if (use_lds)                                                                        \
       hipLaunchKernelGGL((attn_lds_kernel<DP_, DT_>), grid, dim3(256), 0, stream, a);        \
     else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32 && PG_ATTN_WG && DP_ == 256 && \
-             (split_keys == 64 || split_keys == 128 || split_keys == 256)) {                 \
+             (split_keys == 64 || split_keys % 128 == 0)) {                                  \
       if (split_keys == 64)                                                                  \
         hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 2>), grid, dim3(128), 0, stream, a); \
-      else if (split_keys == 128)                                                            \
-        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 4>), grid, dim3(256), 0, stream, a); \
       else                                                                                   \
-        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 8>), grid, dim3(512), 0, stream, a); \
+        hipLaunchKernelGGL((attn_decode_wg_kernel<DP_, DT_, 4>), grid, dim3(256), 0, stream, a); \
     } else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1 && D == DP_ && kcap >= 32)         \
       hipLaunchKernelGGL((attn_decode_kernel<DP_, DT_, true>), grid, dim3(64), 0, stream, a); \
     else if (split_keys > 0 && PG_ATTN_SPLIT_WAVES == 1)                                     \
@@ -781,7 +865,7 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
   AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, (const bf16_t*)k, k_bs, k_hs, k_rs,
              (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, mask, mask_bs, mask_rs,
              Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml,
-             split_keys > 0 ? kcap : 0};
+             split_keys > 0 ? kcap : 0, 0};
   dim3 grid;
   // prefill with >= 1024 one-wave workgroups: the LDS-staged kernel (64 rows per workgroup share K/V);
   // needs 16-B aligned V^T rows / batch offsets
@@ -815,6 +899,14 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
     const int rows = 16 * fa_waves * fa_rpw;
     grid = dim3((Lq * G + rows - 1) / rows, Hkv, B);
     fa_deep = PG_FA_DEEP && fa_waves == 4 && fa_rpw == 1;
+    if (nsplit > 1) {
+      // prefill key split (caller's workspace: part_o [B][Hkv][nsplit][Lq*G][DT*16] fp32, part_ml [..][2])
+      PG_REQUIRE(nsplit <= PF_MAXS && part_o && part_ml && D % 4 == 0);
+      a.pf_splits = nsplit;
+      grid.x *= nsplit;
+    }
+  } else if (split_keys == 0) {
+    PG_REQUIRE(nsplit <= 1);                       // key splits need the flash kernel's shape conditions
   }
   const bool use_lds = fa_waves == 0 && split_keys == 0 && wgs16 >= 1024 && aligned;
   if (fa_waves) {
@@ -837,6 +929,12 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
   ATTN_DISPATCH(256, 16)   // Gemma head_dim 256
   if (!launched) return (int)hipErrorInvalidValue;
   PG_LAUNCH_CHECK();
+  if (a.pf_splits > 1) {
+    const long total = (long)B * Hkv * Lq * G * (D / 4);
+    hipLaunchKernelGGL(attn_pf_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, part_o,
+                       part_ml, nsplit, Lq * G, G, Hkv, D, DT * 16, Lq, (bf16_t*)o, o_rs, total);
+    PG_LAUNCH_CHECK();
+  }
   return 0;
 }
 

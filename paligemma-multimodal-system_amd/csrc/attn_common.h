@@ -17,6 +17,8 @@ struct AttnArgs {
   float* part_ml;          // [B][Hkv][nsplit][16][2]
   int kcap;                // decode: key rows readable per (b, kv head) in K and V^T (the static cache's Smax);
                            // > 0 lets a split issue its first block's loads before the kv length arrives
+  int pf_splits;           // prefill key splits (> 1: attn_fa_kernel writes (O, m, l) partials to part_o / part_ml
+                           // [B][Hkv][pf_splits][Lq*G][DT*16] / [..][2], merged by attn_pf_combine_kernel)
 };
 
 // Branch-free guarded loads: the address is always valid (callers clamp it), the value is

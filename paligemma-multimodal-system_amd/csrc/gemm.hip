@@ -1347,8 +1347,8 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // waves per workgroup of each gemm_tile_kernel shape (4, or 8 / 12 -- see the kernel).  8 / 8 / 8 / 12 measured
 // 3-12 % faster than 4 on every batch-1 prefill GEMM and pt-224 prefill 5.29 -> 4.95 ms
 // (profiles/r03_tile_waves_ab.txt)
-#ifndef PG_TILE_DEEP
-#define PG_TILE_DEEP 0    // 64-row tiles in a one-round grid: deeper staging rings (tuning)
+#ifndef PG_TILE_AUTO_N64
+#define PG_TILE_AUTO_N64 1   // 64 x 64 tiles when the 64 x 128 grid has fewer workgroups than CUs (bf16)
 #endif
 #ifndef PG_TILE_W64
 #define PG_TILE_W64 8
@@ -1368,13 +1368,9 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   if (n64) {
     const int m64 = (e.M + 63) / 64, tn = (e.N + 63) / 64;
     const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
-    // a grid of one round: a 9-stage ring (144 KiB, 8 k-tiles in flight) instead of 4 (64 KiB, 2 workgroups / CU)
-    if (PG_TILE_DEEP && m64 * tn * ksplit <= 256)
-      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 9, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
-                         A, lda, W, ldw, K, kchunk, m64, tn, e);
-    else
-      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
-                         A, lda, W, ldw, K, kchunk, m64, tn, e);
+    // (a 9-stage ring for one-round grids measured 3-10% slower on every batch-1 shape: r03_tile_sweep.txt)
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
+                       A, lda, W, ldw, K, kchunk, m64, tn, e);
     return;
   }
   if constexpr (!F8) {
@@ -1413,9 +1409,12 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   }
   // (a 96-row tile wastes fewer padded rows at M = 264 but measured slower: fewer workgroups)
   const int m64 = (e.M + 63) / 64;
-  if (PG_TILE_DEEP && m64 * tiles_n * ksplit <= 256) {   // one round: 6 stages (144 KiB) instead of 4 (96 KiB)
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 6, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),
-                       dim3(64 * PG_TILE_W64), 0, st, A, lda, W, ldw, K, kchunk, m64, tiles_n, e);
+  if (!F8 && PG_TILE_AUTO_N64 && m64 * tiles_n * ksplit < 256) {
+    // a 64 x 128 grid short of one workgroup per CU: 64 x 64 tiles, twice the workgroups (batch-1 prefill: SigLIP
+    // q|k|v 13.7 -> 11.7 us, never slower on the other shapes; profiles/r03_tile_sweep.txt)
+    const int tn = (e.N + 63) / 64;
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
+                       A, lda, W, ldw, K, kchunk, m64, tn, e);
     return;
   }
   hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),

@@ -90,9 +90,12 @@ class PaliGemmaEngine:
     # (scripts/tune/skinny_bench.py, profiles/r02_skinny_gemm_*.txt): gate/up 60.8 -> 52.8 us, down 38.9 -> 33.5,
     # o 15.2 -> 14.1.  The q|k|v / SigLIP epilogues cannot split K, so their one-tile grids would idle most CUs.
     TILE_M1 = os.environ.get("PG_TILE_M1", "1") != "0"
-    TILE_M1_SPLIT = {"gu": 1, "down": 16, "o": 8}
+    # (o left the table: 64-row tiles at split 3 take 10.3 us against 12.7-13.5 for one row tile at split 8-12,
+    # and leave 3 slabs instead of 8 for the RMSNorm; profiles/r03_tile_sweep.txt)
+    TILE_M1_SPLIT = {"gu": 1, "down": 16}
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
+    DECODE_ONE_ROUND = os.environ.get("PG_DECODE_ONE_ROUND", "1") != "0"   # see _split_keys
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
     # tensor parallel: SigLIP data-parallel over the images when every rank gets at least one (else replicated)
@@ -180,6 +183,7 @@ class PaliGemmaEngine:
         h = self._buf("v_h", (M, w.v_inter), torch.bfloat16)
         s_o = ops.gemm_ksplit(M, hv, hv)
         s_2 = ops.gemm_ksplit(M, hv, w.v_inter)
+        ks_v = self._key_split_args("v", B, N, N, nh, nh, hd)
         part = self._buf("v_part", (max(s_o, s_2), M, hv), torch.float32)
         ns = 0
         for L in w.vl:
@@ -188,7 +192,7 @@ class PaliGemmaEngine:
             ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M + 32,
                      aux_n=2 * hv)
             ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
-                          B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5))
+                          B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5), **ks_v)
             self._gemm_cols(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
             ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
                               nsplit=s_o, out=xn)
@@ -235,6 +239,7 @@ class PaliGemmaEngine:
         s_d = self._ksplit(T, H, I) if T > 16 else self.DECODE_SPLIT_DOWN
         part = self._buf("t_part", (max(s_o, s_d), T, H), torch.float32)
         pos = positions.to(device=self.device, dtype=torch.int32).reshape(-1).contiguous()
+        ks_t = self._key_split_args("t", B, L, L, nh, nkv, hd) if mask is None else {}
         ns = 0
         if taps is not None:
             taps.append(x_resid.clone())
@@ -249,7 +254,7 @@ class PaliGemmaEngine:
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
-                          mask_rs=(mask.stride(-2) if mask is not None else 0))
+                          mask_rs=(mask.stride(-2) if mask is not None else 0), **ks_t)
             n_o = self._row_parallel(attn, Lw, "o", part, T, s_o)
             xin = self._norm(x_resid, Lw["post_w"], part, n_o, xn, T)
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
@@ -264,6 +269,16 @@ class PaliGemmaEngine:
                           row_map=logits_rows, write_resid=False)
         logits = self.lm_head(xf, rows, fresh=True) if want_logits else None
         return logits, hid
+
+    def _key_split_args(self, tag: str, B: int, Lq: int, Lkv: int, Hq: int, Hkv: int, D: int) -> dict:
+        """pg_attention keyword arguments for a key-split prefill attention (ops.prefill_key_splits; {} = unsplit):
+        the split count and its (O, m, l) workspace."""
+        nks = ops.prefill_key_splits(B, Lq, Lkv, Hq, Hkv)
+        if nks <= 1:
+            return {}
+        no, nml = ops.prefill_split_workspace(B, Lq, Hq, Hkv, D, nks)
+        return dict(nsplit=nks, part_o=self._buf(f"pf_po_{tag}", (no,), torch.float32),
+                    part_ml=self._buf(f"pf_pml_{tag}", (nml,), torch.float32))
 
     def _fp8_rows(self, M: int) -> bool:
         return self.fp8 and M > 16
@@ -631,6 +646,11 @@ class PaliGemmaEngine:
         if B <= self.FUSE_MAX_B:
             return self.DECODE_SPLIT_KEYS_SMALL
         blocks = (Smax + SK - 1) // SK
+        if self.DECODE_ONE_ROUND and B * blocks >= 2048:
+            # long KV x batch: 4-wave splits of several 32-key rounds per wave, about 512 workgroups in all (two
+            # resident per CU: one round) -- pt-896 x32: 12 splits of 384 keys instead of 36 of 128 (2.25 rounds)
+            per_batch = max(4, (512 // B) // 4 * 4)
+            return 128 * (-(-Smax // (128 * per_batch)))
         mult = max(1, min(8, (B * blocks) // self.DECODE_SPLIT_TARGET))
         # a power of two: 2 / 4 / 8-block splits run one wave per block, merged in LDS (attn_decode_wg_kernel)
         return SK * (1 << (mult.bit_length() - 1))

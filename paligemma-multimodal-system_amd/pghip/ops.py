@@ -7,6 +7,7 @@ enqueues on torch's current stream.  torch is used only for memory and streams.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -201,6 +202,25 @@ def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *,
               _p(part_o), _p(part_ml), int(kcap), _s())
 
 
+PF_KEYSPLIT = os.environ.get("PG_PF_KEYSPLIT", "1") != "0"
+
+
+def prefill_key_splits(B: int, Lq: int, Lkv: int, Hq: int, Hkv: int) -> int:
+    """Key splits for an unmasked prefill attention whose grid of 64-row workgroups leaves most CUs idle (batch 1:
+    pt-224 Gemma 33 workgroups, SigLIP 64): as many splits (<= 8, >= one 64-key block each) as keep the split grid
+    within one round; 1 = unsplit.  Each split writes (O, m, l) partials that pg_attention merges itself."""
+    wgs = math.ceil(Lq * (Hq // Hkv) / 64) * Hkv * B
+    if not PF_KEYSPLIT or wgs >= 128:
+        return 1
+    return max(1, min(8, 256 // wgs, math.ceil(Lkv / 64)))
+
+
+def prefill_split_workspace(B: int, Lq: int, Hq: int, Hkv: int, D: int, nks: int):
+    """(part_o, part_ml) sizes in fp32 elements for prefill_key_splits' nks splits."""
+    rows = B * Hkv * nks * Lq * (Hq // Hkv)
+    return rows * ((D + 15) // 16 * 16), rows * 2
+
+
 def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
     _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
 
@@ -326,8 +346,10 @@ def slab_sum(part: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 
 def split_for(tiles: int, k_steps: int, target: int = 256, max_split: int = 4) -> int:
-    """split-K factor so that tiles * split >= target, keeping >= 2 k-steps per split."""
-    s = max(1, min(max_split, math.ceil(target / max(tiles, 1)), k_steps // 2))
+    """split-K factor: the most splits with tiles * split <= target (one round of workgroups), keeping >= 2
+    k-steps per split.  (Rounding up to fill every CU measured worse: the Gemma o projection at batch 1, 80 tiles,
+    10.3 us at split 3 vs 14.9 at split 4 -- the fourth split starts a second round; profiles/r03_tile_sweep.txt.)"""
+    s = max(1, min(max_split, target // max(tiles, 1), k_steps // 2))
     return s
 
 
@@ -339,7 +361,7 @@ def gemm_ksplit(M: int, N: int, K: int) -> int:
     Large M (a 256x256 grid of >= 256 tiles, csrc/gemm.hip gemm256_kernel): the split that best fills the
     last round of one-workgroup-per-CU tiles, each extra split charged its partial-slab round trip
     (2*M*N*4 B at ~5 TB/s against 2*M*N*K flop at ~1 PF/s, i.e. 800/K of the GEMM per split).
-    Smaller M: enough 64x128 tiles x splits to reach every CU (split_for)."""
+    Smaller M: as many splits of the 64x128 tiles as keep one round of workgroups (split_for)."""
     t256 = math.ceil(M / 256) * math.ceil(N / 256)
     if t256 >= CUS:
         kt = K // 64

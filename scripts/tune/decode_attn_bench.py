@@ -25,7 +25,7 @@ for name, B, L in (("pt448x16", 16, 1096), ("pt896x32", 32, 4168), ("pt224x1", 1
     lkv = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
     o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
     dt = 256
-    for sk in (32, 64, 128, 256):
+    for sk in (32, 64, 128, 256, 384, 512, 768):
         nsplit = ((Smax + sk - 1) // sk + 3) // 4 * 4
         po = torch.empty(B * nkv * nsplit * 16 * dt, device="cuda")
         pml = torch.empty(B * nkv * nsplit * 16 * 2, device="cuda")

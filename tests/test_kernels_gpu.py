@@ -298,7 +298,7 @@ def test_attention_vision_layout(B, N, nh, hd):
                                                   (2, 4104, 8, 1, 256, False)])                              # pt-896
 def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode, up to the pt-896 prefix
-    (4104 keys: the 2 / 4 / 8-block decode splits of BASELINE configs[4] over 4.2 k keys)."""
+    (4104 keys: the multi-block, multi-round decode splits of BASELINE configs[4] over 4.2 k keys)."""
     from pghip import ops
     Smax = max(320, (L + 8 + 63) // 64 * 64)
     kvd = nkv * hd
@@ -338,9 +338,9 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     ops.attn_combine(po, pml, od, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
     assert err(od, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2
     # kcap = Smax: every split's first block is loaded before the kv length is read (rows past it masked after
-    # the loads land).  One-block splits (32 keys): bit-identical to the kcap = 0 kernel.  2 / 4 / 8-block splits
-    # at head_dim 256 run one wave per block merged in LDS (attn_decode_wg_kernel): same bound as above.
-    for sk in (32, 64, 128, 256):
+    # the loads land).  One-block splits (32 keys): bit-identical to the kcap = 0 kernel.  2- and 4k-block splits
+    # at head_dim 256 run one wave per block, k rounds per wave, merged in LDS (attn_decode_wg_kernel): same bound.
+    for sk in (32, 64, 128, 256, 384, 512):
         ns = ((Smax + sk - 1) // sk + 3) // 4 * 4
         po1 = torch.empty(B * nkv * ns * 16 * dt, device="cuda")
         pml1 = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
@@ -355,6 +355,46 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
             outs.append(od2)
         if sk == 32:
             assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B,L,nh,nkv,hd,nks", [(1, 264, 8, 1, 256, 5), (1, 256, 16, 16, 72, 4),
+                                                (1, 100, 8, 1, 256, 5), (2, 130, 4, 2, 64, 8),
+                                                (1, 264, 8, 1, 256, 0), (1, 256, 16, 16, 72, 0)])
+def test_attention_prefill_key_split(B, L, nh, nkv, hd, nks):
+    """Key-split prefill attention (batch-1 grids: each split walks its share of the 64-key blocks, writes (O, m, l),
+    and pg_attention merges them): against a torch fp32 reference and the unsplit kernel, including splits left
+    without keys (L = 100 in 5 splits of one block).  nks 0 = the engine's policy (ops.prefill_key_splits: 5 for the
+    pt-224 Gemma prefill, 4 for SigLIP)."""
+    from pghip import ops
+    if nks == 0:
+        nks = ops.prefill_key_splits(B, L, L, nh, nkv)
+        assert nks == (5 if hd == 256 else 4)
+    Smax = (L + 8 + 63) // 64 * 64
+    kvd = nkv * hd
+    q = rnd(B * L, nh * hd, seed=71)
+    kc = torch.zeros(B, Smax, kvd, dtype=torch.bfloat16, device="cuda")
+    vtc = torch.zeros(B, kvd, Smax, dtype=torch.bfloat16, device="cuda")
+    kk, vv = rnd(B, L, kvd, seed=72), rnd(B, L, kvd, seed=73)
+    kc[:, :L] = kk
+    vtc[:, :, :L] = vv.transpose(1, 2)
+    args = (q, nh * hd, None, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax)
+    kw = dict(B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5)
+    one = torch.empty(B * L, nh * hd, dtype=torch.bfloat16, device="cuda")
+    ops.attention(*args[:2], one, *args[3:], **kw)
+    no, nml = ops.prefill_split_workspace(B, L, nh, nkv, hd, nks)
+    po = torch.full((no,), float("nan"), device="cuda")
+    pml = torch.full((nml,), float("nan"), device="cuda")
+    split = torch.full_like(one, float("nan"))
+    ops.attention(*args[:2], split, *args[3:], nsplit=nks, part_o=po, part_ml=pml, **kw)
+    g = nh // nkv
+    qh = q.view(B, L, nh, hd).transpose(1, 2)
+    kh = kk.view(B, L, nkv, hd).transpose(1, 2).repeat_interleave(g, 1)
+    vh = vv.view(B, L, nkv, hd).transpose(1, 2).repeat_interleave(g, 1)
+    ref = _attn_ref(qh, kh, vh, hd ** -0.5).transpose(1, 2).reshape(B * L, nh * hd)
+    assert not torch.isnan(split.float()).any()
+    assert err(split, ref) < 2e-2 and err(split, one) < 1e-2
+    with pytest.raises(RuntimeError):                   # more splits than the merge takes
+        ops.attention(*args[:2], split, *args[3:], nsplit=9, part_o=po, part_ml=pml, **kw)
 
 
 def test_rope_kv_write_matches_reference_formula():
