@@ -474,7 +474,8 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
   const int t = threadIdx.x;
-  const int lane = t & 63, wave = t >> 6, c = lane & 15, g = lane >> 4;
+  const int lane = t & 63, c = lane & 15, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform: scalar branches on the piece counts
   const int b = blockIdx.z, kvh = blockIdx.y;
   const int Lkv = a.Lkv;
   const int R = a.Lq * a.G;

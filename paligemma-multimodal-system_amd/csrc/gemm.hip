@@ -332,14 +332,17 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
 // W pieces over the first 8 (12 waves) so every wave's piece count -- its vmcnt step -- is a whole number.
 // BN = 64 (PG_TILE_N64, BM 64 and 4 waves only: 2 x 2 waves of 32 x 32): twice the workgroups of the 64 x 128
 // grid for the small-M prefill GEMMs whose 64 x 128 grid leaves most CUs idle, without a K split.
-template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN>
+// KSUB = 2: a stage holds two 64-k sub-tiles (K % 128 == 0), one barrier / vmcnt wait per 128 k: half the
+// per-k-step synchronisation of the latency-bound small-M tiles.
+template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN, int KSUB = 1>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ W, int ldw, int K,
                                                                int kchunk, int tiles_m, int tiles_n, EpiArgs e) {
   constexpr int A_BYTES = BM * TBK * 2;
   static_assert(BN == TBN || (BN == 64 && BM == 64 && WAVES == 4), "BN 64: 64-row tiles of 4 waves only");
   constexpr int W_BYTES = BN * TBK * 2;
-  constexpr int STAGE_BYTES = A_BYTES + W_BYTES;
+  constexpr int SUB_BYTES = A_BYTES + W_BYTES;
+  constexpr int STAGE_BYTES = KSUB * SUB_BYTES;
   constexpr int WN = BN == 64 ? 2 : (WAVES == 4 ? (BM == 64 ? 4 : 2) : (WAVES == 8 ? (BM == 64 ? 4 : 2) : 2));
   constexpr int WM = WAVES / WN;                   // waves along M
   constexpr int NI = BM / WM / 16;                 // 16-row subtiles per wave
@@ -349,10 +352,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   constexpr int NWW = WAVES > 8 ? 8 : WAVES;       // waves staging W pieces
   __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE_BYTES];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  // wave-uniform (SGPR): the per-wave piece counts and the vmcnt switch below then branch on scalars, not through
+  // an exec-masked chain of every case
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   // glds pieces this wave issues per stage (wave-uniform): its vmcnt step per younger stage in flight
-  const int P = BM / 8 / NWA + (wave < NWW ? BN / 8 / NWW : 0);
+  const int P = KSUB * (BM / 8 / NWA + (wave < NWW ? BN / 8 / NWW : 0));
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped tile order.
   const int nwg = gridDim.x;
@@ -372,7 +377,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   const int z = blockIdx.z;
   const int kbeg = z * kchunk;
   const int kend = min(K, kbeg + kchunk);
-  const int nk = max(0, (kend - kbeg) / TBK);
+  const int nk = max(0, (kend - kbeg) / (TBK * KSUB));
 
   f32x4 acc[NI][NJ];
 #pragma unroll
@@ -383,8 +388,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   auto issue = [&](int kt) {
     char* st = smem + (kt % STAGES) * STAGE_BYTES;
     if (PG_TILE_PROBE == 2) return;                // tuning probe: no loads (MFMA + barrier floor)
-    stage_tile<BM, false, NWA>(A, lda, m0, e.M, kbeg + kt * TBK, st, wave, lane);
-    stage_tile<BN, FRAG, NWW>(W, ldw, n0, e.N, kbeg + kt * TBK, st + A_BYTES, wave, lane);
+#pragma unroll
+    for (int u = 0; u < KSUB; ++u) {
+      const int k0 = kbeg + (kt * KSUB + u) * TBK;
+      stage_tile<BM, false, NWA>(A, lda, m0, e.M, k0, st + u * SUB_BYTES, wave, lane);
+      stage_tile<BN, FRAG, NWW>(W, ldw, n0, e.N, k0, st + u * SUB_BYTES + A_BYTES, wave, lane);
+    }
   };
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -396,7 +405,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
     wait_vm_n(younger * P);
     __builtin_amdgcn_s_barrier();                  // every wave's pieces of kt landed; kt-1 fully read
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
-    const char* tA = smem + (kt % STAGES) * STAGE_BYTES;
+#pragma unroll
+    for (int u = 0; u < KSUB; ++u) {
+    const char* tA = smem + (kt % STAGES) * STAGE_BYTES + u * SUB_BYTES;
     const char* tW = tA + A_BYTES;
     if constexpr (PG_TILE_PROBE == 1) {
       // tuning probe: no fragment reads or MFMAs (the staging pipeline's floor); one LDS word keeps the loads live
@@ -430,6 +441,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 #pragma unroll
           for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(fw[j], fa[i], acc[i][j]);
       }
+    }
     }
   }
 
@@ -1347,6 +1359,9 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // waves per workgroup of each gemm_tile_kernel shape (4, or 8 / 12 -- see the kernel).  8 / 8 / 8 / 12 measured
 // 3-12 % faster than 4 on every batch-1 prefill GEMM and pt-224 prefill 5.29 -> 4.95 ms
 // (profiles/r03_tile_waves_ab.txt)
+#ifndef PG_TILE_KSUB
+#define PG_TILE_KSUB 1    // 2: 64-row tiles stage 128 k per barrier (K % 128 == 0; 3 stages)
+#endif
 #ifndef PG_TILE_AUTO_N64
 #define PG_TILE_AUTO_N64 1   // 64 x 64 tiles when the 64 x 128 grid has fewer workgroups than CUs (bf16)
 #endif
@@ -1362,15 +1377,31 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 #ifndef PG_TILE_W288
 #define PG_TILE_W288 12
 #endif
+// 64-row tiles, BN 128 (WV waves) or 64 (4 waves): 64-k stages (4 deep), or with PG_TILE_KSUB 2 and K % 128 == 0
+// 128-k stages (3 deep)
+template <int EPI, bool FRAG, bool F8, int BN, int WV>
+static void launch_t64(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
+                       hipStream_t st) {
+  const int m64 = (e.M + 63) / 64, tn = (e.N + BN - 1) / BN;
+  if constexpr (PG_TILE_KSUB == 2) {
+    if (K % 128 == 0) {
+      const int kchunk = ((K / 128 + ksplit - 1) / ksplit) * 128;
+      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 3, FRAG, F8, WV, BN, 2>), dim3(m64 * tn, 1, ksplit), dim3(64 * WV),
+                         0, st, A, lda, W, ldw, K, kchunk, m64, tn, e);
+      return;
+    }
+  }
+  const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
+  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, WV, BN>), dim3(m64 * tn, 1, ksplit), dim3(64 * WV), 0, st,
+                     A, lda, W, ldw, K, kchunk, m64, tn, e);
+}
+
 template <int EPI, bool FRAG, bool F8 = false>
 static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st, bool m1 = false, bool n64 = false) {
   if (n64) {
-    const int m64 = (e.M + 63) / 64, tn = (e.N + 63) / 64;
-    const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
     // (a 9-stage ring for one-round grids measured 3-10% slower on every batch-1 shape: r03_tile_sweep.txt)
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
-                       A, lda, W, ldw, K, kchunk, m64, tn, e);
+    launch_t64<EPI, FRAG, F8, 64, 4>(A, lda, W, ldw, K, ksplit, e, st);
     return;
   }
   if constexpr (!F8) {
@@ -1412,14 +1443,10 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   if (!F8 && PG_TILE_AUTO_N64 && m64 * tiles_n * ksplit < 256) {
     // a 64 x 128 grid short of one workgroup per CU: 64 x 64 tiles, twice the workgroups (batch-1 prefill: SigLIP
     // q|k|v 13.7 -> 11.7 us, never slower on the other shapes; profiles/r03_tile_sweep.txt)
-    const int tn = (e.N + 63) / 64;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, 4, 64>), dim3(m64 * tn, 1, ksplit), dim3(256), 0, st,
-                       A, lda, W, ldw, K, kchunk, m64, tn, e);
+    launch_t64<EPI, FRAG, F8, 64, 4>(A, lda, W, ldw, K, ksplit, e, st);
     return;
   }
-  hipLaunchKernelGGL((gemm_tile_kernel<EPI, 64, 4, FRAG, F8, PG_TILE_W64>), dim3(m64 * tiles_n, 1, ksplit),
-                     dim3(64 * PG_TILE_W64), 0, st, A, lda,
-                     W, ldw, K, kchunk, m64, tiles_n, e);
+  launch_t64<EPI, FRAG, F8, TBN, PG_TILE_W64>(A, lda, W, ldw, K, ksplit, e, st);
 }
 
 // measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;

@@ -95,7 +95,10 @@ class PaliGemmaEngine:
     TILE_M1_SPLIT = {"gu": 1, "down": 16}
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
-    DECODE_ONE_ROUND = os.environ.get("PG_DECODE_ONE_ROUND", "1") != "0"   # see _split_keys
+    # long KV x batch: splits of several 32-key rounds per wave sized to one round of workgroups (_split_keys).
+    # Measured level with the 128-key splits (pt-896 x32: 51.8 vs 51.1 us per layer, attention + merge, same box;
+    # profiles/r03_decode_attn_bench.txt), so off
+    DECODE_ONE_ROUND = os.environ.get("PG_DECODE_ONE_ROUND", "0") == "1"
     FIN_MIN_B = 5           # FIN_MIN_B <= B <= 16: in-kernel finalisation with the merge as its own kernel
     USE_FIN = True          # single rank: split-K slabs finalised in-kernel (see _decode_layers_fin)
     # tensor parallel: SigLIP data-parallel over the images when every rank gets at least one (else replicated)
