@@ -949,3 +949,10 @@ extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B,
   PG_LAUNCH_CHECK();
   return 0;
 }
+
+#if PG_ATTN_STAMPS
+// diagnostic variant only (not in the product library): copy the decode-split stamps to the host
+extern "C" int pg_attn_stamps_read(void* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pg_attn_stamp_buf), (size_t)n * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif

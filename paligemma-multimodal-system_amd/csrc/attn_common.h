@@ -3,6 +3,20 @@
 #pragma once
 #include "common.h"
 
+#ifndef PG_VT_PROBE
+#define PG_VT_PROBE 0     // tuning probe only: 1 = V^T blocks read as contiguous 16 KB regions (wrong values)
+#endif
+
+#ifndef PG_ATTN_STAMPS
+#define PG_ATTN_STAMPS 0  // diagnostic variant only: per-wave s_memrealtime stamps of attn_decode_split (FULL)
+#endif
+#if PG_ATTN_STAMPS
+__device__ unsigned long long pg_attn_stamp_buf[8192][4];
+#define PG_STAMP(v) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); v = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PG_STAMP(v) do { } while (0)
+#endif
+
 struct AttnArgs {
   const bf16_t* q; long q_rs;
   bf16_t* o; long o_rs;
@@ -74,6 +88,11 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   const int R = a.Lq * a.G;
   const int D = FULL ? DP : a.D;
   const int kbeg = sp * a.split_keys;
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  (void)st0; (void)st1; (void)st2; (void)st3;
+#if PG_ATTN_STAMPS
+  st0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int r = c;
   const bool rvalid = r < R;
   const int rr = rvalid ? r : (FULL ? R - 1 : 0);
@@ -119,7 +138,12 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const int d = 16 * t + c;
+#if PG_VT_PROBE
+      // timing probe (wrong values): the block's V^T bytes read from one contiguous 16 KB region
+      const bf16_t* vrow = vbase + (long)(kb / 32) * (32 * DP) + (long)(d < D ? d : D - 1) * 32 - kb;
+#else
       const bf16_t* vrow = vbase + (long)(d < D ? d : D - 1) * a.vt_ds;
+#endif
       vr[t][0] = *(const u32x2*)(vrow + kb + 4 * g);
       vr[t][1] = *(const u32x2*)(vrow + kb + 16 + 4 * g);
     }
@@ -194,6 +218,7 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   if constexpr (FULL) {
     // the prefetched first block runs unconditionally (straight-line from its loads: nothing for hipcc to sink
     // below a kv-length branch), later blocks of a multi-block split load as they go
+    PG_STAMP(st1);
     block(kbeg);
     for (int kb = kbeg + 32; kb < kend; kb += 32) {
       load_block(kb, kend, kfa, kfb, vr);
@@ -207,6 +232,10 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   }
   // lane holds O^T[d = 16t + 4g + j][q = c]
   const long base = (((long)b * a.Hkv + kvh) * nsplit + sp) * 16 + c;
+#if PG_ATTN_STAMPS
+  asm volatile("" :: "v"(o[0][0]), "v"(o[DT - 1][3]));
+  st2 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (!rvalid) return;                       // rows past Lq*G are never merged
   float* po = a.part_o + base * (DT * 16);
 #pragma unroll
@@ -223,6 +252,16 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
       a.part_ml[base * 2 + 1] = l;
     }
   }
+#if PG_ATTN_STAMPS
+  PG_STAMP(st3);
+  if (lane == 0) {
+    const int id = (b * a.Hkv + kvh) * nsplit + sp;
+    if (id < 8192) {
+      pg_attn_stamp_buf[id][0] = st0; pg_attn_stamp_buf[id][1] = st1;
+      pg_attn_stamp_buf[id][2] = st2; pg_attn_stamp_buf[id][3] = st3;
+    }
+  }
+#endif
 }
 
 // One 32-key block [kb, kb + 32) of a decode split, one wave, head_dim == DP, known cache capacity (a.kcap >= 32):
@@ -260,7 +299,11 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
     }
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
+#if PG_VT_PROBE
+      const bf16_t* vrow = vbase + (long)(kl / 32) * (32 * DP) + (long)(16 * t + c) * 32 - kl;
+#else
       const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
+#endif
       vr[t][0] = *(const u32x2*)(vrow + kl + 4 * g);
       vr[t][1] = *(const u32x2*)(vrow + kl + 16 + 4 * g);
     }
