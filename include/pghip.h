@@ -21,7 +21,8 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 4: the measured-slower decode variants and their PgFusedArgs fields removed */
+int pg_abi_version(void);   /* 5: pg_attn_decode (batched decode attention + merge, one launch); 4: the
+                              measured-slower decode variants and their PgFusedArgs fields removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
  * Returns hipErrorInvalidValue (truncated) when n < 65. */
@@ -140,6 +141,17 @@ int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, lo
                  int kcap, hipStream_t stream);
 int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                     void* o, long o_rs, hipStream_t stream);
+
+/* Batched split-KV decode attention with the split merge in the same launch (gemma.py:307-339 for one new position
+ * per row; replaces pg_attention(split) + pg_attn_combine for B > 2, ABI 5).  The kcap/32 cache blocks of a
+ * (batch, kv head) are dealt round-robin to nsplit splits of nw (2 or 4) waves, nb rounds each (nw*nsplit <=
+ * kcap/32 <= nw*nsplit*nb); the last-arriving split (one agent-scope ticket in counters[b*Hkv + kvh], left zero)
+ * merges the partials and writes o[b][hq][0..D) bf16.  D = 32 or 256.  The cache must hold finite values in every
+ * row below kcap (masked keys get weight 0 but their V is not zeroed). */
+int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs, long k_rs,
+                   const void* vt, long vt_bs, long vt_hs, long vt_ds, int B, int Lkv, const int* lkv_dev, int Hq,
+                   int Hkv, int D, float scale, int kcap, int nsplit, int nw, int nb, float* part_o, float* part_ml,
+                   int* counters, hipStream_t stream);
 
 /* RoPE (gemma.py:112-151) on q in place and k; k -> cache rows, v -> transposed cache (KVCache.update
  * gemma.py:18-57 as a static in-place append). */

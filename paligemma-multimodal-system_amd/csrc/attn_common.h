@@ -3,9 +3,6 @@
 #pragma once
 #include "common.h"
 
-#ifndef PG_VT_PROBE
-#define PG_VT_PROBE 0     // tuning probe only: 1 = V^T blocks read as contiguous 16 KB regions (wrong values)
-#endif
 
 #ifndef PG_ATTN_STAMPS
 #define PG_ATTN_STAMPS 0  // diagnostic variant only: per-wave s_memrealtime stamps of attn_decode_split (FULL)
@@ -50,6 +47,19 @@ static __device__ __forceinline__ u32x2 ld_vt4(const bf16_t* row, int key, int k
   const uint32_t lo = nv >= 2 ? v[0] : (nv == 1 ? (v[0] & 0xFFFFu) : 0u);
   const uint32_t hi = nv >= 4 ? v[1] : (nv == 3 ? (v[1] & 0xFFFFu) : 0u);
   return u32x2{lo, hi};
+}
+
+// Split-KV decode key order inside a 32-key block: MFMA row i of the first S^T half is key 8(i/4) + i%4, of the
+// second 8(i/4) + 4 + i%4, so lane (c, g) ends up holding the scores of keys 8g..8g+7 -- P^T is 8 consecutive keys
+// per lane and each V^T row is read as one 16-B chunk (keys 8g..8g+7) instead of two 8-B pieces: a load instruction
+// covers 16 rows x 64 B of V^T, not 16 x 32 B (scripts/tune/kv_pattern.hip, pt-896 x32 decode shapes: the cache read
+// alone 42.6 -> 30.5 us per layer).  The K rows are loaded in that order (any row order is free for K).
+static __device__ __forceinline__ int dec_krow(int c) { return 8 * (c >> 2) + (c & 3); }
+
+// a V^T chunk of 8 consecutive keys with the keys from the n-th on zeroed (n = valid keys in the chunk)
+static __device__ __forceinline__ u32x4 vmask8(u32x4 v, int n) {
+  return u32x4{n >= 2 ? v[0] : (n == 1 ? (v[0] & 0xFFFFu) : 0u), n >= 4 ? v[1] : (n == 3 ? (v[1] & 0xFFFFu) : 0u),
+               n >= 6 ? v[2] : (n == 5 ? (v[2] & 0xFFFFu) : 0u), n >= 8 ? v[3] : (n == 7 ? (v[3] & 0xFFFFu) : 0u)};
 }
 
 typedef __attribute__((address_space(1))) unsigned long long pg_gu64;
@@ -120,8 +130,8 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   float m = -INFINITY, l = 0.f;
   // raw loads of one 32-key block: K rows for S^T (rows clamped below rowcap), 4-key runs of the V^T rows
   // (row padded to a multiple of 32 keys); masking by the kv length is applied after the loads land
-  auto load_block = [&](int kb, int rowcap, u32x4 (&kfa)[KS], u32x4 (&kfb)[KS], u32x2 (&vr)[DT][2]) {
-    const int ka = min(kb + c, rowcap - 1), kbk = min(kb + 16 + c, rowcap - 1);
+  auto load_block = [&](int kb, int rowcap, u32x4 (&kfa)[KS], u32x4 (&kfb)[KS], u32x4 (&vr)[DT]) {
+    const int ka = min(kb + dec_krow(c), rowcap - 1), kbk = min(kb + dec_krow(c) + 4, rowcap - 1);
     const bf16_t* pa = kbase + (long)ka * a.k_rs;
     const bf16_t* pb = kbase + (long)kbk * a.k_rs;
 #pragma unroll
@@ -138,14 +148,8 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const int d = 16 * t + c;
-#if PG_VT_PROBE
-      // timing probe (wrong values): the block's V^T bytes read from one contiguous 16 KB region
-      const bf16_t* vrow = vbase + (long)(kb / 32) * (32 * DP) + (long)(d < D ? d : D - 1) * 32 - kb;
-#else
       const bf16_t* vrow = vbase + (long)(d < D ? d : D - 1) * a.vt_ds;
-#endif
-      vr[t][0] = *(const u32x2*)(vrow + kb + 4 * g);
-      vr[t][1] = *(const u32x2*)(vrow + kb + 16 + 4 * g);
+      vr[t] = *(const u32x4*)(vrow + kb + 8 * g);
     }
   };
   // decode with a known cache capacity: the first block is in flight before the kv length is read.  FULL
@@ -153,7 +157,7 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   // never used -- so no branch joins the loads (hipcc's wait bookkeeping stays exact)
   const bool pre = FULL || (a.kcap > 0 && kbeg < a.kcap);
   u32x4 kfa[KS], kfb[KS];
-  u32x2 vr[DT][2];
+  u32x4 vr[DT];
   if (FULL) load_block(min(kbeg, a.kcap - 32), a.kcap, kfa, kfb, vr);
   else if (pre) load_block(kbeg, a.kcap, kfa, kfb, vr);
   const int Lkv = (FULL ? __builtin_amdgcn_readfirstlane(lkv_raw) : (a.lkv_dev ? *a.lkv_dev : 0)) + a.Lkv;
@@ -168,13 +172,7 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
       const bool dok = 16 * t + c < D;
-      const int k0 = kb + 4 * g, k1 = kb + 16 + 4 * g;
-      const int n0 = dok ? kend - k0 : 0, n1 = dok ? kend - k1 : 0;   // valid keys among each run of 4
-      const u32x2 v0 = vr[t][0], v1 = vr[t][1];
-      vf[t] = u32x4{n0 >= 2 ? v0[0] : (n0 == 1 ? (v0[0] & 0xFFFFu) : 0u),
-                    n0 >= 4 ? v0[1] : (n0 == 3 ? (v0[1] & 0xFFFFu) : 0u),
-                    n1 >= 2 ? v1[0] : (n1 == 1 ? (v1[0] & 0xFFFFu) : 0u),
-                    n1 >= 4 ? v1[1] : (n1 == 3 ? (v1[1] & 0xFFFFu) : 0u)};
+      vf[t] = vmask8(vr[t], dok ? kend - (kb + 8 * g) : 0);   // keys 8g..8g+7 of the block
     }
     f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -185,9 +183,8 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     float x[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k0 = kb + 4 * g + j, k1 = kb + 16 + 4 * g + j;
-      x[j] = k0 < kend ? sA[j] * a.scale_log2 : -INFINITY;
-      x[4 + j] = k1 < kend ? sB[j] * a.scale_log2 : -INFINITY;
+      x[j] = kb + 8 * g + j < kend ? sA[j] * a.scale_log2 : -INFINITY;
+      x[4 + j] = kb + 8 * g + 4 + j < kend ? sB[j] * a.scale_log2 : -INFINITY;
     }
     float bm = x[0];
 #pragma unroll
@@ -288,10 +285,10 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   // a block past the cache reads the last block (never used: all its keys are masked)
   const int kl = min(kb, a.kcap - 32);
   u32x4 kfa[KS], kfb[KS];
-  u32x2 vr[DT][2];
+  u32x4 vr[DT];
   {
-    const bf16_t* pa = kbase + (long)(kl + c) * a.k_rs;
-    const bf16_t* pb = kbase + (long)(kl + 16 + c) * a.k_rs;
+    const bf16_t* pa = kbase + (long)(kl + dec_krow(c)) * a.k_rs;
+    const bf16_t* pb = kbase + (long)(kl + dec_krow(c) + 4) * a.k_rs;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       kfa[s] = *(const u32x4*)(pa + 32 * s + 8 * g);
@@ -299,13 +296,8 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
     }
 #pragma unroll
     for (int t = 0; t < DT; ++t) {
-#if PG_VT_PROBE
-      const bf16_t* vrow = vbase + (long)(kl / 32) * (32 * DP) + (long)(16 * t + c) * 32 - kl;
-#else
       const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
-#endif
-      vr[t][0] = *(const u32x2*)(vrow + kl + 4 * g);
-      vr[t][1] = *(const u32x2*)(vrow + kl + 16 + 4 * g);
+      vr[t] = *(const u32x4*)(vrow + kl + 8 * g);
     }
   }
   // every load of the block is issued before its first use (one memory round trip)
@@ -314,14 +306,7 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   const int kend = min(Lkv, kb + 32);
   u32x4 vf[DT];
 #pragma unroll
-  for (int t = 0; t < DT; ++t) {
-    const int n0 = kend - (kb + 4 * g), n1 = kend - (kb + 16 + 4 * g);   // valid keys among each run of 4
-    const u32x2 v0 = vr[t][0], v1 = vr[t][1];
-    vf[t] = u32x4{n0 >= 2 ? v0[0] : (n0 == 1 ? (v0[0] & 0xFFFFu) : 0u),
-                  n0 >= 4 ? v0[1] : (n0 == 3 ? (v0[1] & 0xFFFFu) : 0u),
-                  n1 >= 2 ? v1[0] : (n1 == 1 ? (v1[0] & 0xFFFFu) : 0u),
-                  n1 >= 4 ? v1[1] : (n1 == 3 ? (v1[1] & 0xFFFFu) : 0u)};
-  }
+  for (int t = 0; t < DT; ++t) vf[t] = vmask8(vr[t], kend - (kb + 8 * g));   // keys 8g..8g+7
   f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -331,8 +316,8 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   float x[8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    x[j] = kb + 4 * g + j < kend ? sA[j] * a.scale_log2 : -INFINITY;
-    x[4 + j] = kb + 16 + 4 * g + j < kend ? sB[j] * a.scale_log2 : -INFINITY;
+    x[j] = kb + 8 * g + j < kend ? sA[j] * a.scale_log2 : -INFINITY;
+    x[4 + j] = kb + 8 * g + 4 + j < kend ? sB[j] * a.scale_log2 : -INFINITY;
   }
   float bm = x[0];
 #pragma unroll
@@ -355,4 +340,97 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, f32x4{0.f, 0.f, 0.f, 0.f});
+}
+
+// ---- batched decode (attn_decode_fused_kernel): one 32-key block's loads, and its online-softmax update ----
+
+// K rows [kb, kb + 32) and V^T runs of kv head (kbase / vbase), rows clamped below the cache capacity: a block past
+// the kv length is read anyway (the last cache block at worst) and masked after its loads land, so the loads of a
+// round are unconditional and hipcc's wait counting stays exact (head_dim == DP).
+template <int DP, int DT>
+__device__ __forceinline__ void dec_load_block(const AttnArgs& a, const bf16_t* kbase, const bf16_t* vbase, int kb,
+                                               int c, int g, u32x4 (&kfa)[DP / 32], u32x4 (&kfb)[DP / 32],
+                                               u32x4 (&vr)[DT]) {
+  const int kl = min(kb, a.kcap - 32);
+  const bf16_t* pa = kbase + (long)(kl + dec_krow(c)) * a.k_rs;
+  const bf16_t* pb = kbase + (long)(kl + dec_krow(c) + 4) * a.k_rs;
+#pragma unroll
+  for (int s = 0; s < DP / 32; ++s) {
+    kfa[s] = *(const u32x4*)(pa + 32 * s + 8 * g);
+    kfb[s] = *(const u32x4*)(pb + 32 * s + 8 * g);
+  }
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
+    vr[t] = *(const u32x4*)(vrow + kl + 8 * g);
+  }
+}
+
+// (o, m, l) <- the online-softmax update with the loaded block [kb, kb + 32), keys >= kend masked (the arithmetic of
+// attn_decode_split's block).  S^T = K.Q^T keeps a row's statistics lane-local; P feeds O^T = V^T.P^T from the S
+// accumulators, the key order inside the k-step permuted identically for V^T (lane holds keys 4g.., 16 + 4g..).
+// MASK_V = false: V^T past kend is not zeroed (P is 0 there already): only for caches that hold finite values in every
+// row (the engine's zero-initialised static cache, written only with model outputs) -- saves 64 registers.
+template <int DP, int DT, bool MASK_V = true>
+__device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int kend, int c, int g,
+                                                 const bf16x8 (&qf)[DP / 32], const u32x4 (&kfa)[DP / 32],
+                                                 const u32x4 (&kfb)[DP / 32], const u32x4 (&vr)[DT],
+                                                 f32x4 (&o)[DT], float& m, float& l) {
+  (void)c;
+  u32x4 vf[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    if constexpr (MASK_V)
+      vf[t] = vmask8(vr[t], kend - (kb + 8 * g));   // keys 8g..8g+7
+    else
+      vf[t] = vr[t];
+  }
+  f32x4 sA = {0.f, 0.f, 0.f, 0.f}, sB = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < DP / 32; ++s) {
+    sA = mfma16(__builtin_bit_cast(bf16x8, kfa[s]), qf[s], sA);
+    sB = mfma16(__builtin_bit_cast(bf16x8, kfb[s]), qf[s], sB);
+  }
+  float x[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[j] = kb + 8 * g + j < kend ? sA[j] * scale_log2 : -INFINITY;
+    x[4 + j] = kb + 8 * g + 4 + j < kend ? sB[j] * scale_log2 : -INFINITY;
+  }
+  float bm = x[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
+  bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
+  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  const float mn = fmaxf(m, bm);
+  const bool none = mn == -INFINITY;          // every key so far masked
+  const float alpha = none ? 1.f : exp2f(m - mn);
+  float rs = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  l = l * alpha + rs;
+  m = mn;
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] *= alpha;
+  u32x4 pw;
+  pw[0] = pack_bf2(x[0], x[1]);
+  pw[1] = pack_bf2(x[2], x[3]);
+  pw[2] = pack_bf2(x[4], x[5]);
+  pw[3] = pack_bf2(x[6], x[7]);
+  const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, o[t]);
+}
+
+// 16-byte write-through (sc1) store / load through a buffer resource (MI355X guide: in-launch hand-off, R1 form)
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t pg_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+static __device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, byte_off, 0, 16);
+}
+static __device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16));
 }

@@ -40,6 +40,8 @@ SIGNATURES = {
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
                      i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp],
     "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
+    "pg_attn_decode": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, i32, i32, vp, i32, i32, i32, f32, i32,
+                       i32, i32, i32, vp, vp, vp, vp],
     "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],
     "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],
     "pg_image_rank": [vp, i32, i64, vp, vp],
@@ -72,7 +74,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 def source_hash(lib=None) -> str:

@@ -92,7 +92,7 @@ class PaliGemmaEngine:
     TILE_M1 = os.environ.get("PG_TILE_M1", "1") != "0"
     # (o left the table: 64-row tiles at split 3 take 10.3 us against 12.7-13.5 for one row tile at split 8-12,
     # and leave 3 slabs instead of 8 for the RMSNorm; profiles/r03_tile_sweep.txt)
-    TILE_M1_SPLIT = {"gu": 1, "down": 16}
+    TILE_M1_SPLIT = {"gu": 1, "down": int(os.environ.get("PG_M1_DOWN", "16"))}
     FUSE_MAX_B = 2          # decode batches up to this size fuse RMSNorm / attention merge into the GEMVs
     DECODE_SPLIT_TARGET = 1024  # B > FUSE_MAX_B: aim for about this many decode-attention splits (waves)
     # long KV x batch: splits of several 32-key rounds per wave sized to one round of workgroups (_split_keys).
@@ -108,6 +108,8 @@ class PaliGemmaEngine:
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
+    # B > FUSE_MAX_B: split-KV attention and its merge in one launch (pg_attn_decode; 0 = split kernel + combine)
+    DECODE_FUSED_ATTN = os.environ.get("PG_DECODE_FUSED", "1") != "0"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -496,8 +498,9 @@ class PaliGemmaEngine:
         SK = self._split_keys(B, cache.Smax)
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
         dt = (hd + 15) // 16 * 16
-        part_o = self._buf("d_po", (B * nkv * nsplit * 16 * dt,), torch.float32)
-        part_ml = self._buf("d_pml", (B * nkv * nsplit * 16 * 2,), torch.float32)
+        ns_ws = max(nsplit, ops.decode_plan(B, nkv, cache.Smax)[0]) if B > self.FUSE_MAX_B else nsplit
+        part_o = self._buf("d_po", (B * nkv * ns_ws * 16 * dt,), torch.float32)
+        part_ml = self._buf("d_pml", (B * nkv * ns_ws * 16 * 2,), torch.float32)
         chain = bool(st.get("chain")) and self._chain_ok(sampler)
         if not chain:                               # chained: the previous sample() wrote res_a already
             ops.embed_merge(st["ids"], None, w.embed, feats, feats.shape[0] if feats is not None else 0, res_a,
@@ -563,6 +566,27 @@ class PaliGemmaEngine:
             self.sample(logits, st, sampler, advance=True, feats=feats)
         return logits
 
+    def _decode_attn_merged(self, i, st, cache, qb, attn, part_o, part_ml, SK, nsplit):
+        """Split-KV decode attention of layer i for B > FUSE_MAX_B rows, merged into attn bf16 [B][nh*hd]: one
+        pg_attn_decode launch (DECODE_FUSED_ATTN), else the split kernel + pg_attn_combine."""
+        w = self.w
+        B = qb.shape[0]
+        nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
+        kvd = nkv * hd
+        if self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64:
+            ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                            cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                            B=B, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
+                            kcap=cache.Smax, part_o=part_o, part_ml=part_ml,
+                            counters=self._zeros("d_dec_cnt", (B * nkv,), torch.int32))
+            return
+        ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                      cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                      B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                      scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
+                      part_ml=part_ml, kcap=cache.Smax)
+        ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+
     def _split_o(self, B: int) -> int:
         if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
             return self.DECODE_SPLIT_O_SMALL
@@ -612,19 +636,19 @@ class PaliGemmaEngine:
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
                 ops.gemm_fused(xq, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
-            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
-                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                          part_ml=part_ml, kcap=cache.Smax)
             if merge_in_gemv:
+                ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+                              cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+                              B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
+                              scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
+                              part_ml=part_ml, kcap=cache.Smax)
                 fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                     head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                     akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
                                     norm_w=Lw["post_w"])
                 ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             else:
-                ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+                self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK, nsplit)
                 fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
                                     norm_w=Lw["post_w"])
                 ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
@@ -675,12 +699,7 @@ class PaliGemmaEngine:
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv)
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
-            ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                          cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
-                          B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
-                          scale=1.0 / math.sqrt(hd), split_keys=SK or self.DECODE_SPLIT_KEYS, nsplit=nsplit,
-                          part_o=part_o, part_ml=part_ml, kcap=cache.Smax)
-            ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+            self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS, nsplit)
             self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
             self._allreduce(part[:so])
             xin = self._norm(res, Lw["post_w"], part, so, xn, B)

@@ -225,6 +225,35 @@ def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
     _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
 
 
+def decode_plan(B: int, Hkv: int, kcap: int, cus: int = 256):
+    """(nsplit, nw, nb) of pg_attn_decode for a batch of B rows over a static cache of kcap keys: about one workgroup
+    per CU (measured: pt-896 x32, 8 splits x 4 waves x 5 rounds 38.6 us per layer vs 42.4 at 16 splits x 3 rounds, two
+    workgroups per CU; scripts/tune/decode_attn_bench.py), the kcap/32 blocks of a (row, kv head) dealt round-robin
+    to its splits; 4 waves per split when every wave of one workgroup per CU gets a block, else 2; at most 16 splits,
+    the partials the last split merges in one round trip."""
+    nblk = kcap // 32
+    rows = max(1, B * Hkv)
+    nw = 4 if rows * nblk >= 4 * cus else 2
+    s_max = max(1, min(16, cus // rows))
+    nsplit = max(1, min(s_max, nblk // nw))
+    nb = -(-nblk // (nw * nsplit))
+    return nsplit, nw, nb
+
+
+def attn_decode(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale,
+                kcap, part_o, part_ml, counters, plan=None):
+    """Batched decode attention with the split merge in the same launch (pg_attn_decode): o[b][hq*D + d] bf16 from
+    q (one position per row) over the static cache; part_o / part_ml / counters are workspaces (counters int32 [B*Hkv],
+    zeroed once)."""
+    nsplit, nw, nb = plan or decode_plan(B, Hkv, kcap)
+    if part_o.numel() < B * Hkv * nsplit * 16 * D or part_ml.numel() < B * Hkv * nsplit * 16 * 2:
+        raise ValueError("pghip.attn_decode: partial workspace too small")
+    if counters.dtype != torch.int32 or counters.numel() < B * Hkv:
+        raise ValueError("pghip.attn_decode: counters must be int32 [B*Hkv]")
+    _lib.call("pg_attn_decode", _p(q), q_rs, _p(o), o_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds, B, Lkv,
+              _p(lkv_dev), Hq, Hkv, D, float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _s())
+
+
 def rope_kv_write(qkv, pos, cos_t, sin_t, kc, vtc, *, T, L, Hq, Hkv, D, Smax, slot_base=0, slot_dev=None):
     _chk(qkv, torch.bfloat16, "qkv")
     _chk(pos, torch.int32, "pos")

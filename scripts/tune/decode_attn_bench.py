@@ -25,6 +25,47 @@ for name, B, L in (("pt448x16", 16, 1096), ("pt896x32", 32, 4168), ("pt224x1", 1
     lkv = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
     o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
     dt = 256
+    # the fused kernel (pg_attn_decode: attention + merge in one launch) at its default plan and neighbours
+    cnt = torch.zeros(B * nkv, dtype=torch.int32, device="cuda")
+    nblk = Smax // 32
+    plans = [ops.decode_plan(B, nkv, Smax)]
+    for nw, ns in ((2, 8), (2, 16), (4, 8), (4, 16), (4, 4), (4, 6), (4, 11), (4, 24), (4, 33), (2, 19), (4, 10),
+                   (4, 5), (4, 3)):
+        if nw * ns <= nblk and (ns, nw, -(-nblk // (nw * ns))) not in plans:
+            plans.append((ns, nw, -(-nblk // (nw * ns))))
+    for plan in plans:
+        po = torch.empty(B * nkv * plan[0] * 16 * 256, device="cuda")
+        pml = torch.empty(B * nkv * plan[0] * 16 * 2, device="cuda")
+
+        def layer(i, plan=plan, po=po, pml=pml):
+            ops.attn_decode(q, nh * hd, o, nh * hd, kc[i], Smax * kvd, hd, kvd, vtc[i], kvd * Smax, hd * Smax, Smax,
+                            B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=Smax, part_o=po,
+                            part_ml=pml, counters=cnt, plan=plan)
+        layer(0)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                for i in range(layers):
+                    layer(i)
+        g.replay()
+        torch.cuda.synchronize()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(5):
+            g.replay()
+        ev[1].record()
+        torch.cuda.synchronize()
+        us = ev[0].elapsed_time(ev[1]) * 1000 / (5 * layers)
+        kv_bytes = B * L * kvd * 2 * 2
+        res[f"{name}/fused{plan}"] = round(us, 2)
+        print(f"{name} fused plan {plan}: {us:7.2f} us per layer (attention + merge), "
+              f"{kv_bytes / us / 1e3:7.1f} GB/s of KV", flush=True)
+    if os.environ.get("PG_FUSED_ONLY"):
+        del kc, vtc
+        continue
     for sk in (32, 64, 128, 256, 384, 512, 768):
         nsplit = ((Smax + sk - 1) // sk + 3) // 4 * 4
         po = torch.empty(B * nkv * nsplit * 16 * dt, device="cuda")

@@ -177,8 +177,11 @@ def test_pt224_full_size_teacher_forced_decode(golden):
     the graph-free decode step is fed the reference's tokens (teacher forcing) and its logits are compared
     with the reference's top-64 logits of every step.  Bound: max error on those 64 logits < 15% of their
     scale (the synthetic model's intrinsic bf16 sensitivity is ~10%, see test_pt224_full_size_parity), and
-    the top-1 id must equal the reference's at every step whose top1-top2 margin exceeds twice that
-    step's measured error (bf16 cannot order closer pairs reliably)."""
+    the top-1 id must equal the reference's at every step whose reference top1-top2 margin exceeds 0.5 logits:
+    twice this recipe's per-logit bf16 error (0.21-0.44 measured per step, scripts/tune/tf_errors.py; bf16 cannot
+    order closer pairs reliably).  The checked steps are fixed by the golden (4 of 16), not by the run's own error,
+    so a rounding-order change in a kernel cannot move a step out of the check.  The bit-exact greedy check is
+    test_pt224_free_running_greedy_ids_equal_reference (better-conditioned recipe)."""
     from pghip import configs, engine, synthetic, weights
     g = golden("pt224")
     cfg = configs.PT_224
@@ -199,10 +202,11 @@ def test_pt224_full_size_teacher_forced_decode(golden):
         top_ids, top_v = g["step_top64_ids"][t], g["step_top64_values"][t]
         e = float(np.abs(lg[top_ids] - top_v).max())
         assert e < 0.15 * float(np.abs(top_v).max()), (t, e)
-        if g["margin"][t] > 2 * e:
+        if g["margin"][t] > 0.5:
+            assert e < 0.5 * float(g["margin"][t]) + 0.05, (t, e, float(g["margin"][t]))
             assert int(np.argmax(lg)) == int(g["greedy_ids"][t]), (t, e, float(g["margin"][t]))
             checked += 1
-    assert checked >= 4, checked
+    assert checked == int((g["margin"] > 0.5).sum()) == 4, checked
 
 
 def test_batched_generation_per_row_eos(tiny, golden):

@@ -357,6 +357,54 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
             assert torch.equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("B,L,nh,nkv,hd,kcap", [(3, 200, 8, 1, 256, 256), (4, 40, 4, 1, 32, 64),
+                                                 (5, 300, 8, 2, 256, 448),                # GQA: 2 kv heads
+                                                 (16, 1033, 8, 1, 256, 1216),             # pt-448 x16 decode
+                                                 (32, 4169, 8, 1, 256, 4224),             # pt-896 x32 decode
+                                                 (8, 97, 8, 1, 256, 128)])
+def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
+    """pg_attn_decode (split-KV attention + in-launch merge, B > 2) against fp32 softmax attention over the first L
+    cached keys; rows past L hold finite stale values (the static cache after a longer request), every split plan
+    (2 / 4 waves, 1..16 splits, several rounds) agrees, repeated calls are bit-identical and leave the tickets zero."""
+    from pghip import ops
+    kvd = nkv * hd
+    q = rnd(B, nh * hd, seed=31)
+    kc = rnd(B, kcap, kvd, seed=32)                  # stale finite rows past L
+    vtc = rnd(B, kvd, kcap, seed=33)
+    lkv = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
+    g = nh // nkv
+    kf = kc[:, :L].float().view(B, L, nkv, hd).transpose(1, 2).repeat_interleave(g, 1)       # [B][nh][L][hd]
+    vf = vtc[:, :, :L].float().view(B, nkv, hd, L).transpose(2, 3).repeat_interleave(g, 1)
+    ref = _attn_ref(q.view(B, nh, 1, hd), kf, vf, hd ** -0.5).reshape(B, nh * hd)
+    cnt = torch.zeros(B * nkv, dtype=torch.int32, device="cuda")
+    nblk = kcap // 32
+    plans = {ops.decode_plan(B, nkv, kcap)}
+    for nw in (2, 4):
+        for ns in (1, 3, 16):
+            if nw * ns <= nblk:
+                plans.add((ns, nw, -(-nblk // (nw * ns))))
+    outs = {}
+    for plan in sorted(plans):
+        ns = plan[0]
+        po = torch.empty(B * nkv * ns * 16 * hd, device="cuda")
+        pml = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
+        o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
+        for rep in range(2):
+            ops.attn_decode(q, nh * hd, o, nh * hd, kc, kcap * kvd, hd, kvd, vtc, kvd * kcap, hd * kcap, kcap,
+                            B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=kcap, part_o=po,
+                            part_ml=pml, counters=cnt, plan=plan)
+            torch.cuda.synchronize()
+            assert int(cnt.abs().sum()) == 0, plan
+            if rep == 0:
+                first = o.clone()
+        assert torch.equal(first, o), plan
+        assert err(o, ref) < 2e-2, plan
+        outs[plan] = o
+    base = next(iter(outs.values()))
+    for plan, o in outs.items():
+        assert err(o, base.float()) < 1e-2, plan
+
+
 @pytest.mark.parametrize("B,L,nh,nkv,hd,nks", [(1, 264, 8, 1, 256, 5), (1, 256, 16, 16, 72, 4),
                                                 (1, 100, 8, 1, 256, 5), (2, 130, 4, 2, 64, 8),
                                                 (1, 264, 8, 1, 256, 0), (1, 256, 16, 16, 72, 0)])
