@@ -124,10 +124,11 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
 }
 
 // Batched decode (B > 2: the batch alone fills the chip) with the split merge in the same launch.
-// One workgroup of NW waves per (split, kv head, batch).  The 32-key blocks of the cache are dealt to the S splits
-// round-robin (block i -> split i % S; inside a split, round j of wave w takes its (4j + w)-th block), so every
-// split gets the same number of blocks whatever the cache length, and S is chosen so that two workgroups sit on
-// every CU (pg_attn_decode's caller): one workgroup's loads overlap the other's compute.  The NW running (O, m, l)
+// One workgroup of NW waves per (split, kv head, batch).  The cache is dealt to the S splits in granules of NW
+// consecutive 32-key blocks, round-robin (granule i -> split i % S; round j of a split takes its j-th granule, wave
+// w its w-th block), so every split gets the same number of blocks whatever the cache length and the two 64-B
+// halves of a 128-B V^T line (adjacent blocks) are read by one CU (dealing single blocks round-robin put them on
+// two XCDs, each fetching the whole line).  The NW running (O, m, l)
 // merge through LDS into the split's partial, stored write-through (sc1); one agent-scope ticket per (batch,
 // kv head) then makes the workgroup of the last-arriving split merge the S partials (sc1 loads: the MI355X guide's
 // in-launch hand-off with no release / acquire fence) and write the bf16 attention rows -- no combine launch.
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   float m = -INFINITY, l = 0.f;
   // round 0 (every split owns at least NW blocks: nsplit <= kcap / 128): its loads are issued before the kv length
   // arrives; later rounds skip blocks past the cache (wave-uniform)
-  int blk = sp + S * wave;
+  int blk = sp * NW + wave;
   dec_load_block<DP, DT>(a, kbase, vbase, 32 * blk, c, g, kfa, kfb, vr);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -185,11 +186,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   {
     bf16x8 qf[KS];
     qfrag(qf);
-    dec_block_update<DP, DT, false>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr, o, m,
-                                    l);
+    dec_block_update<DP, DT, false, true>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr,
+                                          o, m, l);
   }
   for (int j = 1; j < nb; ++j) {
-    blk = sp + S * (NW * j + wave);
+    blk = (sp + S * j) * NW + wave;
     if (blk >= nblk) break;
     dec_load_block<DP, DT>(a, kbase, vbase, 32 * blk, c, g, kfa, kfb, vr);
     __builtin_amdgcn_sched_barrier(0);

@@ -2,6 +2,7 @@
 // one-wave split-KV decode block.
 #pragma once
 #include "common.h"
+#include <type_traits>
 
 
 #ifndef PG_ATTN_STAMPS
@@ -164,7 +165,9 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   const int kend = min(Lkv, kbeg + a.split_keys);
   // one 32-key block from the loaded registers: mask by the kv length, S^T, online softmax, P.V.  A block with
   // no valid key (a peeled first block past the kv length) leaves (o, m, l) = (0, -inf, 0) untouched.
-  auto block = [&](int kb) {
+  // first = the split's first block: (o, m, l) are still (0, -inf, 0), so O needs no rescale (64 multiplies of
+  // accumulator registers skipped: a one-block split -- batch-1 decode -- never rescales)
+  auto block = [&](int kb, auto first) {
     // every load of the block is issued before its first use (one memory round trip): the scheduler would
     // otherwise sink the V^T loads below the S^T MFMAs, behind the K loads' wait
     __builtin_amdgcn_sched_barrier(0);
@@ -199,10 +202,14 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
     m = mn;
+    if constexpr (decltype(first)::value) {
+      l = rs;
+    } else {
+      l = l * alpha + rs;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+      for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    }
     u32x4 pw;
     pw[0] = pack_bf2(x[0], x[1]);
     pw[1] = pack_bf2(x[2], x[3]);
@@ -212,19 +219,21 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
 #pragma unroll
     for (int t = 0; t < DT; ++t) o[t] = mfma16(__builtin_bit_cast(bf16x8, vf[t]), pf, o[t]);
   };
+  using first_t = std::integral_constant<bool, true>;
+  using later_t = std::integral_constant<bool, false>;
   if constexpr (FULL) {
     // the prefetched first block runs unconditionally (straight-line from its loads: nothing for hipcc to sink
     // below a kv-length branch), later blocks of a multi-block split load as they go
     PG_STAMP(st1);
-    block(kbeg);
+    block(kbeg, first_t{});
     for (int kb = kbeg + 32; kb < kend; kb += 32) {
       load_block(kb, kend, kfa, kfb, vr);
-      block(kb);
+      block(kb, later_t{});
     }
   } else {
     for (int kb = kbeg; kb < kend; kb += 32) {
       if (!pre || kb != kbeg) load_block(kb, kend, kfa, kfb, vr);
-      block(kb);
+      block(kb, later_t{});
     }
   }
   // lane holds O^T[d = 16t + 4g + j][q = c]
@@ -371,7 +380,7 @@ __device__ __forceinline__ void dec_load_block(const AttnArgs& a, const bf16_t* 
 // accumulators, the key order inside the k-step permuted identically for V^T (lane holds keys 4g.., 16 + 4g..).
 // MASK_V = false: V^T past kend is not zeroed (P is 0 there already): only for caches that hold finite values in every
 // row (the engine's zero-initialised static cache, written only with model outputs) -- saves 64 registers.
-template <int DP, int DT, bool MASK_V = true>
+template <int DP, int DT, bool MASK_V = true, bool FIRST = false>
 __device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int kend, int c, int g,
                                                  const bf16x8 (&qf)[DP / 32], const u32x4 (&kfa)[DP / 32],
                                                  const u32x4 (&kfb)[DP / 32], const u32x4 (&vr)[DT],
@@ -410,10 +419,14 @@ __device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int k
   for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
   rs += __shfl_xor(rs, 16, 64);
   rs += __shfl_xor(rs, 32, 64);
-  l = l * alpha + rs;
   m = mn;
+  if constexpr (FIRST) {                        // (o, m, l) = (0, -inf, 0): nothing to rescale
+    l = rs;
+  } else {
+    l = l * alpha + rs;
 #pragma unroll
-  for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+  }
   u32x4 pw;
   pw[0] = pack_bf2(x[0], x[1]);
   pw[1] = pack_bf2(x[2], x[3]);

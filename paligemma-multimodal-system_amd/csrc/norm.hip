@@ -10,13 +10,14 @@
 #include "common.h"
 
 #define NORM_MAXV 4   // float4 per thread -> H <= 4096
-#ifndef NORM_SG
-#define NORM_SG 8     // split-K slabs loaded per round
-#endif
+// Split-K slabs loaded per round (SG) and float4 slots per thread (MAXV) are template parameters: 8 slabs per round
+// pays where few rows carry many slabs (batch-1 prefill: 16-slab down projection), but its 214 registers (two
+// waves per SIMD) tripled the 16 k-row norms of pt-448 x16 (55 -> 151 us each, 85 -> 93 ms per prefill): large
+// launches take 2 slabs per round and the H <= 2048 slot count (pg_norm_residual picks).
 
 // Q8: y goes out as fp8 e4m3 bytes (out = uint8 [M][ldo]) with its row scale in out_f32[orow] (the
 // pg_quant_fp8 rule applied to the bf16-rounded y, so the bytes equal quantising the bf16 output).
-template <bool Q8>
+template <bool Q8, int NORM_SG, int MAXV>
 __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ resid, const float* __restrict__ partials,
                                                             int nsplit, int M_part, const float* __restrict__ w,
                                                             const float* __restrict__ b, bf16_t* __restrict__ out,
@@ -29,27 +30,29 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   const int H4 = H >> 2;
   const int nv = (H4 + 255) >> 8;                  // float4 slots in use per thread (wave-uniform)
   float* x = resid + (size_t)row * H;
-  f32x4 v[NORM_MAXV];
+  f32x4 v[MAXV];
   // the residual and the split-K slabs, NORM_SG slabs per round with every load of a round issued before the
-  // first add (slab indices past nsplit re-read the last slab, columns past H the last column; both are dropped
-  // after the loads): one memory round trip per round instead of one per slab (the runtime-bounded add loop
-  // waited for each slab's load before issuing the next -- SigLIP's 6-slab LayerNorm took 6.9 us)
+  // first add (columns past H re-read the last column, dropped after the loads): one memory round trip per round
+  // instead of one per slab (the runtime-bounded add loop waited for each slab's load before issuing the next --
+  // SigLIP's 6-slab LayerNorm took 6.9 us).  Slabs past nsplit are not loaded (wave-uniform guard): re-reading the
+  // last slab in their place multiplied a one-slab norm's L2 reads by NORM_SG at pt-448 x16 (135 MB slabs)
 #pragma unroll
-  for (int i = 0; i < NORM_MAXV; ++i)
+  for (int i = 0; i < MAXV; ++i)
     if (i < nv) v[i] = ((const f32x4*)x)[min((int)threadIdx.x + i * 256, H4 - 1)];
   for (int s0 = 0; s0 < nsplit; s0 += NORM_SG) {
-    f32x4 p[NORM_MAXV][NORM_SG];
+    f32x4 p[MAXV][NORM_SG];
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i)
+    for (int i = 0; i < MAXV; ++i)
       if (i < nv) {
         const int c = min((int)threadIdx.x + i * 256, H4 - 1);
 #pragma unroll
         for (int k = 0; k < NORM_SG; ++k)
-          p[i][k] = ((const f32x4*)(partials + ((size_t)min(s0 + k, nsplit - 1) * M_part + row) * H))[c];
+          p[i][k] = s0 + k < nsplit ? ((const f32x4*)(partials + ((size_t)(s0 + k) * M_part + row) * H))[c]
+                                    : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i)
+    for (int i = 0; i < MAXV; ++i)
       if (i < nv) {
 #pragma unroll
         for (int k = 0; k < NORM_SG; ++k)
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
       }
   }
 #pragma unroll
-  for (int i = 0; i < NORM_MAXV; ++i) {
+  for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * 256;
     if (c >= H4 || i >= nv) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     else if (write_resid && nsplit > 0) ((f32x4*)x)[c] = v[i];
@@ -66,11 +69,11 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   if (mode == 0) {
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    for (int i = 0; i < MAXV; ++i) s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
     mean = block_sum(s, red) / (float)H;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i) {
+    for (int i = 0; i < MAXV; ++i) {
       const int c = threadIdx.x + i * 256;
       if (c < H4) {
 #pragma unroll
@@ -81,14 +84,14 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   } else {
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i)
+    for (int i = 0; i < MAXV; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) q += v[i][j] * v[i][j];
     rstd = rsqrtf(block_sum(q, red) / (float)H + eps);
   }
   float amax = 0.f;
 #pragma unroll
-  for (int i = 0; i < NORM_MAXV; ++i) {
+  for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * 256;
     if (c < H4) {
       const f32x4 wv = ((const f32x4*)w)[c];
@@ -129,7 +132,7 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
     if (threadIdx.x == 0) out_f32[orow] = sc;
     uint8_t* q = (uint8_t*)out + (size_t)orow * ldo;
 #pragma unroll
-    for (int i = 0; i < NORM_MAXV; ++i) {
+    for (int i = 0; i < MAXV; ++i) {
       const int c = threadIdx.x + i * 256;
       if (c < H4) {
         float t[4];
@@ -143,6 +146,22 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   }
 }
 
+template <bool Q8>
+static void norm_launch(int M_out, int H, int nsplit, hipStream_t stream, float* resid, const float* partials,
+                        int M_part, const float* w, const float* b, void* out, int ldo, float* out_f32,
+                        const int* row_map, int mode, float eps, int write_resid) {
+  const bool deep = nsplit > 2 && M_out <= 2048;      // few rows, many slabs: one round trip per 8 slabs
+  const bool wide = H > 2048;
+#define PG_NORM_GO(SG_, MV_)                                                                                    \
+  hipLaunchKernelGGL((norm_residual_kernel<Q8, SG_, MV_>), dim3(M_out), dim3(256), 0, stream, resid, partials,   \
+                     nsplit, M_part, w, b, (bf16_t*)out, ldo, out_f32, row_map, H, mode, eps, write_resid)
+  if (deep && wide) PG_NORM_GO(8, 4);
+  else if (deep) PG_NORM_GO(8, 2);
+  else if (wide) PG_NORM_GO(2, 4);
+  else PG_NORM_GO(2, 2);
+#undef PG_NORM_GO
+}
+
 // mode: 0 = LayerNorm (w, b), 1 = Gemma RMSNorm (1 + w).  partials: [nsplit][M_part][H] (may be null).
 // row_map (optional, device int32 [M_out]): output row i normalises input row row_map[i].
 extern "C" int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part, const float* w,
@@ -151,8 +170,8 @@ extern "C" int pg_norm_residual(float* resid, const float* partials, int nsplit,
   PG_REQUIRE(M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV);
   PG_REQUIRE(mode == 1 || b != nullptr);
   PG_REQUIRE(nsplit == 0 || partials != nullptr);
-  hipLaunchKernelGGL(norm_residual_kernel<false>, dim3(M_out), dim3(256), 0, stream, resid, partials, nsplit, M_part,
-                     w, b, (bf16_t*)out, ldo, out_f32, row_map, H, mode, eps, write_resid);
+  norm_launch<false>(M_out, H, nsplit, stream, resid, partials, M_part, w, b, out, ldo, out_f32, row_map, mode, eps,
+                     write_resid);
   PG_LAUNCH_CHECK();
   return 0;
 }
@@ -166,8 +185,8 @@ extern "C" int pg_norm_residual_fp8(float* resid, const float* partials, int nsp
              ldq >= H && ldq % 4 == 0);
   PG_REQUIRE(mode == 1 || b != nullptr);
   PG_REQUIRE(nsplit == 0 || partials != nullptr);
-  hipLaunchKernelGGL(norm_residual_kernel<true>, dim3(M_out), dim3(256), 0, stream, resid, partials, nsplit, M_part,
-                     w, b, (bf16_t*)q, ldq, scale, row_map, H, mode, eps, write_resid);
+  norm_launch<true>(M_out, H, nsplit, stream, resid, partials, M_part, w, b, q, ldq, scale, row_map, mode, eps,
+                    write_resid);
   PG_LAUNCH_CHECK();
   return 0;
 }

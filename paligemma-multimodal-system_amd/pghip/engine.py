@@ -110,6 +110,7 @@ class PaliGemmaEngine:
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
     # B > FUSE_MAX_B: split-KV attention and its merge in one launch (pg_attn_decode; 0 = split kernel + combine)
     DECODE_FUSED_ATTN = os.environ.get("PG_DECODE_FUSED", "1") != "0"
+    FUSED_MIN_ROUNDS = int(os.environ.get("PG_FUSED_MIN_ROUNDS", "3"))   # ... used from this many rounds per split on
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -573,7 +574,11 @@ class PaliGemmaEngine:
         B = qb.shape[0]
         nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
-        if self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64:
+        # the one-launch kernel where the cache needs several rounds of waves (pt-896 x32: 34.3 vs 43.3 us per layer,
+        # attention + merge); with one or two rounds its last split's serial merge of every partial (64-152 KB read
+        # by one CU) costs what the combine launch does (pt-448 x16: 14.6 vs 13.6-13.8 us; profiles/r03_decode_attn_plans.txt)
+        if (self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64
+                and ops.decode_plan(B, nkv, cache.Smax)[2] >= self.FUSED_MIN_ROUNDS):
             ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                             cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                             B=B, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
