@@ -21,8 +21,8 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 5: pg_attn_decode (batched decode attention + merge, one launch); 4: the
-                              measured-slower decode variants and their PgFusedArgs fields removed */
+int pg_abi_version(void);   /* 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+                              them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
  * Returns hipErrorInvalidValue (truncated) when n < 65. */
@@ -84,6 +84,9 @@ typedef struct PgFusedArgs {
   int slab_rows;            /* PG_EPI_F32 split-K: rows between slabs (slab z of row m at C + (z*slab_rows + m)*ldc);
                                0 = M.  Lets a GEMM be issued as row blocks that write into one [ksplit][rows][N]
                                partial tensor (C pointing at the block's first row)                            */
+  void* kd;                 /* PG_EPI_QKV_ROPE (ABI 6, may be null): decode-order copies of the cache, [B][Hkv][Smax][D]
+                               each, written beside kc / vtc (element offsets: csrc/attn_common.h dec_koff / dec_voff) */
+  void* vd;
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -133,12 +136,13 @@ int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part
 /* Flash attention (bidirectional unless an additive mask is given; MQA/GQA by row stacking).
  * siglip.py:96-136 ; gemma.py:307-339 (repeat_kv :185-196 eliminated).  split_keys > 0: decode
  * split-KV partials, merge with pg_attn_combine; kcap > 0 = readable cache rows (Smax, multiple of 32): each split's
- * first block is loaded before the kv length is read (ABI 2). */
+ * first block is loaded before the kv length is read (ABI 2), and (D a multiple of 32) K and V are read from the
+ * decode-order copies kd / vd the QKV epilogue writes (PgFusedArgs.kd / vd, ABI 6; null otherwise). */
 int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
                  long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
                  long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
                  int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
-                 int kcap, hipStream_t stream);
+                 int kcap, const void* kd, const void* vd, hipStream_t stream);
 int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                     void* o, long o_rs, hipStream_t stream);
 
@@ -148,10 +152,9 @@ int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, in
  * kcap/32 <= nw*nsplit*nb); the last-arriving split (one agent-scope ticket in counters[b*Hkv + kvh], left zero)
  * merges the partials and writes o[b][hq][0..D) bf16.  D = 32 or 256.  The cache must hold finite values in every
  * row below kcap (masked keys get weight 0 but their V is not zeroed). */
-int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs, long k_rs,
-                   const void* vt, long vt_bs, long vt_hs, long vt_ds, int B, int Lkv, const int* lkv_dev, int Hq,
-                   int Hkv, int D, float scale, int kcap, int nsplit, int nw, int nb, float* part_o, float* part_ml,
-                   int* counters, hipStream_t stream);
+int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* kd, const void* vd, int B, int Lkv,
+                   const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit, int nw, int nb,
+                   float* part_o, float* part_ml, int* counters, hipStream_t stream);
 
 /* RoPE (gemma.py:112-151) on q in place and k; k -> cache rows, v -> transposed cache (KVCache.update
  * gemma.py:18-57 as a static in-place append). */

@@ -157,8 +157,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
     qv[k] = *(const u32x4*)(qrow0 + (long)min(i / (DP / 8), G - 1) * DP + 8 * (i % (DP / 8)));
   }
   __builtin_amdgcn_sched_barrier(0);               // (the q loads stay ahead of the K/V stream)
-  const bf16_t* kbase = a.k + (long)b * a.k_bs + (long)kvh * a.k_hs;
-  const bf16_t* vbase = a.vt + (long)b * a.vt_bs + (long)kvh * a.vt_hs;
+  const bf16_t* kbase = a.kd + ((long)b * a.Hkv + kvh) * a.kcap * DP;   // decode-order copies
+  const bf16_t* vbase = a.vd + ((long)b * a.Hkv + kvh) * a.kcap * DP;
   const int nblk = a.kcap >> 5;
   auto qfrag = [&](bf16x8 (&qf)[KS]) {
 #pragma unroll
@@ -1020,21 +1020,24 @@ static void launch_fa(int waves, int rpw, bool deep, dim3 grid, hipStream_t stre
 // split_keys == 0: prefill mode (writes bf16 o).  split_keys > 0: decode mode, Lq*Hq/Hkv <= 16, nsplit partials
 // (nsplit multiple of 4) to part_o / part_ml, then call pg_attn_combine.  kcap > 0 (decode): K rows and V^T
 // columns [0, kcap) are readable (a static cache's Smax, a multiple of 32), so each split issues its first block's
-// loads before the kv length arrives from lkv_dev; 0 = rows clamped to the kv length.
+// loads before the kv length arrives from lkv_dev; 0 = rows clamped to the kv length.  Decode with kcap > 0 and
+// D a multiple of 32 reads K and V only from the decode-order copies kd / vd ([B][Hkv][kcap][D], ABI 6).
 extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
                             long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, const float* mask,
                             long mask_bs, long mask_rs, int B, int Lq, int Lkv, const int* lkv_dev, int Hq, int Hkv,
                             int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
-                            int kcap, hipStream_t stream) {
+                            int kcap, const void* kd, const void* vd, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && D > 0 && D % 8 == 0 && D <= 256);
   PG_REQUIRE(kcap >= 0 && kcap % 32 == 0);
   const int G = Hq / Hkv;
   const int DP = ((D + 31) / 32) * 32;
   const int DT = (D + 15) / 16;
+  if (split_keys > 0 && kcap >= 32 && D == DP)
+    PG_REQUIRE(kd && vd && ((uintptr_t)kd & 15) == 0 && ((uintptr_t)vd & 15) == 0);
   AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, (const bf16_t*)k, k_bs, k_hs, k_rs,
              (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, mask, mask_bs, mask_rs,
              Lq, Lkv, G, Hkv, D, lkv_dev, scale * 1.4426950408889634f, split_keys, part_o, part_ml,
-             split_keys > 0 ? kcap : 0, 0};
+             split_keys > 0 ? kcap : 0, 0, (const bf16_t*)kd, (const bf16_t*)vd};
   dim3 grid;
   // prefill with >= 1024 one-wave workgroups: the LDS-staged kernel (64 rows per workgroup share K/V);
   // needs 16-B aligned V^T rows / batch offsets
@@ -1121,25 +1124,23 @@ extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B,
 }
 
 // Batched split-KV decode with the merge in the same launch (attn_decode_fused_kernel): o[b][hq][:] (bf16, row stride
-// o_rs per batch row) from q (one position per batch row), the static cache (K [..][kcap][D] rows, V^T [..][D][kcap],
-// strides as pg_attention) and the device kv length Lkv + *lkv_dev.  The kcap / 32 blocks of 32 keys are dealt to
-// nsplit splits per (batch, kv head) round-robin, to nw (2 or 4) waves per split, at most nw * nb per split
-// (nw * nsplit <= kcap / 32 <= nw * nsplit * nb); workspace part_o [B][Hkv][nsplit][16][D], part_ml [B][Hkv][nsplit][16][2] fp32; counters int32 [B * Hkv],
-// zero before the first call (every call leaves them zero).  head_dim 32 or 256, D == head_dim.
-extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* k, long k_bs, long k_hs,
-                              long k_rs, const void* vt, long vt_bs, long vt_hs, long vt_ds, int B, int Lkv,
-                              const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit, int nw,
-                              int nb, float* part_o, float* part_ml, int* counters, hipStream_t stream) {
+// o_rs per batch row) from q (one position per batch row) over the decode-order cache copies kd / vd ([B][Hkv][kcap][D],
+// dec_koff / dec_voff) and the device kv length Lkv + *lkv_dev.  The kcap / 32 blocks of 32 keys are dealt to nsplit
+// splits per (batch, kv head) in granules of nw (2 or 4) blocks, nb rounds each (nw * nsplit <= kcap / 32 <=
+// nw * nsplit * nb); workspace part_o [B][Hkv][nsplit][16][D], part_ml [B][Hkv][nsplit][16][2] fp32; counters int32
+// [B * Hkv], zero before the first call (every call leaves them zero).  head_dim 32 or 256, D == head_dim.
+extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* kd, const void* vd, int B,
+                              int Lkv, const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit,
+                              int nw, int nb, float* part_o, float* part_ml, int* counters, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && (D == 32 || D == 256));
   PG_REQUIRE((nw == 2 || nw == 4) && kcap % 32 == 0 && nsplit >= 1 && nw * nsplit <= kcap / 32 && nb >= 1 &&
-             nsplit * nw * nb >= kcap / 32 && part_o && part_ml && counters && o && lkv_dev);
+             nsplit * nw * nb >= kcap / 32 && part_o && part_ml && counters && o && lkv_dev && kd && vd);
   PG_REQUIRE((long)B * Hkv * nsplit * 16 * D * 4 < 0x7fffffffL);
-  PG_REQUIRE(q_rs % 8 == 0 && k_rs % 8 == 0 && k_bs % 8 == 0 && k_hs % 8 == 0 && vt_ds % 8 == 0 && vt_bs % 8 == 0 &&
-             vt_hs % 8 == 0 && o_rs % 8 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)k & 15) == 0 &&
-             ((uintptr_t)vt & 15) == 0 && ((uintptr_t)o & 15) == 0);
-  AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, (const bf16_t*)k, k_bs, k_hs, k_rs,
-             (const bf16_t*)vt, vt_bs, vt_hs, vt_ds, nullptr, 0, 0,
-             1, Lkv, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, 32 * 4 * nb, part_o, part_ml, kcap, 0};
+  PG_REQUIRE(q_rs % 8 == 0 && o_rs % 8 == 0 && ((uintptr_t)q & 15) == 0 && ((uintptr_t)kd & 15) == 0 &&
+             ((uintptr_t)vd & 15) == 0 && ((uintptr_t)o & 15) == 0);
+  AttnArgs a{(const bf16_t*)q, q_rs, (bf16_t*)o, o_rs, nullptr, 0, 0, 0, nullptr, 0, 0, 0, nullptr, 0, 0,
+             1, Lkv, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, 32 * 4 * nb, part_o, part_ml, kcap, 0,
+             (const bf16_t*)kd, (const bf16_t*)vd};
   const dim3 grid(nsplit, Hkv, B);
   if (D == 256 && nw == 4)
     hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 4>), grid, dim3(256), 0, stream, a, nb, counters);

@@ -31,7 +31,34 @@ struct AttnArgs {
                            // > 0 lets a split issue its first block's loads before the kv length arrives
   int pf_splits;           // prefill key splits (> 1: attn_fa_kernel writes (O, m, l) partials to part_o / part_ml
                            // [B][Hkv][pf_splits][Lq*G][DT*16] / [..][2], merged by attn_pf_combine_kernel)
+  const bf16_t* kd;        // decode-order cache copies [B][Hkv][kcap][D] (dec_koff / dec_voff): the kcap > 0 decode
+  const bf16_t* vd;        // kernels read K and V only from these
 };
+
+// Decode-order copies of the static KV cache (ABI 6).  The QKV epilogue writes every appended k / v twice: to the
+// canonical K [.][Smax][D] / V^T [.][D][Smax] (prefill attention, the reference KVCache views) and to these copies,
+// laid out so that every load instruction of a decode split reads one contiguous KiB (scripts/tune/kv_pattern.hip:
+// the cache read of pt-896 x32, 30.5 us per layer as 16 rows x 64 B per instruction, 22.8 us as 1 KB).  Per 32-key
+// block, 16 KB each (D = 256):
+//   K: [half h][D/8 chunks][16 MFMA rows][8 dims]; row r of half h is key 8(r/4) + 4h + r%4 (dec_krow's order), so
+//      the (half, k-step s) fragment -- chunks 4s..4s+3 of 16 rows -- is 1 KB;
+//   V: [D/16 d-tiles][4 key groups g][16 dims][8 keys 8g..8g+7], so the d-tile t fragment of V^T is 1 KB.
+static __device__ __forceinline__ long dec_koff(int k, int d, int D) {
+  const int blk = k >> 5, kk = k & 31, h = (kk >> 2) & 1, r = ((kk >> 3) << 2) | (kk & 3);
+  return ((((long)blk * 2 + h) * (D >> 3) + (d >> 3)) * 16 + r) * 8 + (d & 7);
+}
+static __device__ __forceinline__ long dec_voff(int k, int d, int D) {
+  const int blk = k >> 5, kk = k & 31;
+  return ((((long)blk * (D >> 4) + (d >> 4)) * 4 + (kk >> 3)) * 16 + (d & 15)) * 8 + (kk & 7);
+}
+// a lane's 16-B fragment pieces: K half h, k-step s of block kl (lane (c, g): chunk 4s + g of MFMA row c), and the
+// V^T d-tile t of block kl (lane (c, g): keys 8g..8g+7 of dim 16t + c)
+static __device__ __forceinline__ long dec_kfrag(int kl, int h, int s, int c, int g, int D) {
+  return ((((long)(kl >> 5) * 2 + h) * (D >> 3) + 4 * s + g) * 16 + c) * 8;
+}
+static __device__ __forceinline__ long dec_vfrag(int kl, int t, int c, int g, int D) {
+  return ((((long)(kl >> 5) * (D >> 4) + t) * 4 + g) * 16 + c) * 8;
+}
 
 // Branch-free guarded loads: the address is always valid (callers clamp it), the value is
 // zeroed by selects.  Conditional loads compiled to branches and, for partial blocks, to
@@ -131,7 +158,19 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
   float m = -INFINITY, l = 0.f;
   // raw loads of one 32-key block: K rows for S^T (rows clamped below rowcap), 4-key runs of the V^T rows
   // (row padded to a multiple of 32 keys); masking by the kv length is applied after the loads land
+  const bf16_t* kdb = FULL ? a.kd + ((long)b * a.Hkv + kvh) * a.kcap * DP : nullptr;
+  const bf16_t* vdb = FULL ? a.vd + ((long)b * a.Hkv + kvh) * a.kcap * DP : nullptr;
   auto load_block = [&](int kb, int rowcap, u32x4 (&kfa)[KS], u32x4 (&kfb)[KS], u32x4 (&vr)[DT]) {
+    if constexpr (FULL) {     // decode-order copies: one contiguous KiB per load instruction (block kb < kcap)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        kfa[s] = *(const u32x4*)(kdb + dec_kfrag(kb, 0, s, c, g, DP));
+        kfb[s] = *(const u32x4*)(kdb + dec_kfrag(kb, 1, s, c, g, DP));
+      }
+#pragma unroll
+      for (int t = 0; t < DT; ++t) vr[t] = *(const u32x4*)(vdb + dec_vfrag(kb, t, c, g, DP));
+      return;
+    }
     const int ka = min(kb + dec_krow(c), rowcap - 1), kbk = min(kb + dec_krow(c) + 4, rowcap - 1);
     const bf16_t* pa = kbase + (long)ka * a.k_rs;
     const bf16_t* pb = kbase + (long)kbk * a.k_rs;
@@ -296,18 +335,17 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   u32x4 kfa[KS], kfb[KS];
   u32x4 vr[DT];
   {
-    const bf16_t* pa = kbase + (long)(kl + dec_krow(c)) * a.k_rs;
-    const bf16_t* pb = kbase + (long)(kl + dec_krow(c) + 4) * a.k_rs;
+    (void)kbase;
+    (void)vbase;
+    const bf16_t* kdb = a.kd + ((long)b * a.Hkv + kvh) * a.kcap * DP;
+    const bf16_t* vdb = a.vd + ((long)b * a.Hkv + kvh) * a.kcap * DP;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      kfa[s] = *(const u32x4*)(pa + 32 * s + 8 * g);
-      kfb[s] = *(const u32x4*)(pb + 32 * s + 8 * g);
+      kfa[s] = *(const u32x4*)(kdb + dec_kfrag(kl, 0, s, c, g, DP));
+      kfb[s] = *(const u32x4*)(kdb + dec_kfrag(kl, 1, s, c, g, DP));
     }
 #pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
-      vr[t] = *(const u32x4*)(vrow + kl + 8 * g);
-    }
+    for (int t = 0; t < DT; ++t) vr[t] = *(const u32x4*)(vdb + dec_vfrag(kl, t, c, g, DP));
   }
   // every load of the block is issued before its first use (one memory round trip)
   __builtin_amdgcn_sched_barrier(0);
@@ -353,26 +391,22 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
 
 // ---- batched decode (attn_decode_fused_kernel): one 32-key block's loads, and its online-softmax update ----
 
-// K rows [kb, kb + 32) and V^T runs of kv head (kbase / vbase), rows clamped below the cache capacity: a block past
-// the kv length is read anyway (the last cache block at worst) and masked after its loads land, so the loads of a
-// round are unconditional and hipcc's wait counting stays exact (head_dim == DP).
+// K and V^T fragments of the 32-key block at kb from the decode-order copies of one (row, kv head) (kbase / vbase:
+// a.kd / a.vd at that head), the block clamped below the cache capacity: a block past the kv length is read anyway
+// (the last cache block at worst) and masked after its loads land, so the loads of a round are unconditional and
+// hipcc's wait counting stays exact (head_dim == DP).
 template <int DP, int DT>
 __device__ __forceinline__ void dec_load_block(const AttnArgs& a, const bf16_t* kbase, const bf16_t* vbase, int kb,
                                                int c, int g, u32x4 (&kfa)[DP / 32], u32x4 (&kfb)[DP / 32],
                                                u32x4 (&vr)[DT]) {
   const int kl = min(kb, a.kcap - 32);
-  const bf16_t* pa = kbase + (long)(kl + dec_krow(c)) * a.k_rs;
-  const bf16_t* pb = kbase + (long)(kl + dec_krow(c) + 4) * a.k_rs;
 #pragma unroll
   for (int s = 0; s < DP / 32; ++s) {
-    kfa[s] = *(const u32x4*)(pa + 32 * s + 8 * g);
-    kfb[s] = *(const u32x4*)(pb + 32 * s + 8 * g);
+    kfa[s] = *(const u32x4*)(kbase + dec_kfrag(kl, 0, s, c, g, DP));
+    kfb[s] = *(const u32x4*)(kbase + dec_kfrag(kl, 1, s, c, g, DP));
   }
 #pragma unroll
-  for (int t = 0; t < DT; ++t) {
-    const bf16_t* vrow = vbase + (long)(16 * t + c) * a.vt_ds;
-    vr[t] = *(const u32x4*)(vrow + kl + 8 * g);
-  }
+  for (int t = 0; t < DT; ++t) vr[t] = *(const u32x4*)(vbase + dec_vfrag(kl, t, c, g, DP));
 }
 
 // (o, m, l) <- the online-softmax update with the loaded block [kb, kb + 32), keys >= kend masked (the arithmetic of

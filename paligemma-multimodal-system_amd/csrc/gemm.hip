@@ -85,6 +85,10 @@ struct PgFusedArgs {
   const float* a_scale;      // [M]
   const float* w_scale;      // [N] (in W's row order, e.g. the packed q|k|v or interleaved gate/up rows)
   int slab_rows;             // PG_EPI_F32 split-K: rows between slabs (0 = M); lets a GEMM run as row blocks
+  // PG_EPI_QKV_ROPE (optional, ABI 6): the decode-order copies of the cache (kd / vd, attn_common.h dec_koff /
+  // dec_voff), [B][Hkv][Smax][D] each: every appended k / v is also written there
+  bf16_t* kd;
+  bf16_t* vd;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -160,12 +164,19 @@ __device__ __forceinline__ void epi_qkv_rope4_core(const EpiArgs& e, int m, int 
       *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + blk * D + d0) = pk;
     } else if (in_cache) {
       *(u32x2*)(f.kc + ((size_t)b * f.smax + slot) * KV + (blk - Hq) * D + d0) = pk;
+      if (f.kd)     // 4 dims of one key: 8 contiguous bytes of one 16-B chunk
+        *(u32x2*)(f.kd + ((size_t)b * Hkv + (blk - Hq)) * f.smax * D + dec_koff(slot, d0, D)) = pk;
     }
   } else {
     const int c0 = (blk - Hq - Hkv) * D + d0;
     if (in_cache) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) f.vtc[((size_t)b * KV + c0 + j) * f.smax + slot] = f2bf(v[j]);
+      if (f.vd) {
+        bf16_t* vd = f.vd + ((size_t)b * Hkv + (blk - Hq - Hkv)) * f.smax * D;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) vd[dec_voff(slot, d0 + j, D)] = f2bf(v[j]);
+      }
     }
   }
 }

@@ -68,8 +68,7 @@ class KVCache:
             new = KVStore(nl, B, _rup(max(need, 2 * st.Smax if need > st.Smax else st.Smax), 64), st.kv_dim,
                           st.k.device)
             n = max(self._len) if self._len else 0
-            new.k[:st.k.shape[0], :, :n] = st.k[:, :, :n]
-            new.vt[:st.k.shape[0], :, :, :n] = st.vt[:, :, :, :n]
+            new.copy_prefix_from(st, n)
             self._store = new
             self._len += [0] * (nl - len(self._len))
             self.layers = nl
@@ -96,6 +95,10 @@ class KVCache:
         st.k[layer_idx, :, cur:cur + L] = k.to(st.k.dtype)
         st.vt[layer_idx, :, :, cur:cur + L] = value_states.transpose(1, 2).reshape(B, L, nkv * hd).transpose(1, 2).to(
             st.vt.dtype)
+        if hd % 16 == 0:                          # the decode-order copies the engine's decode kernels read
+            kd, vd = ops.decode_cache_pack(st.k[layer_idx], st.vt[layer_idx], nkv)
+            st.kd[layer_idx].copy_(kd.reshape(-1))
+            st.vd[layer_idx].copy_(vd.reshape(-1))
         self._len[layer_idx] = cur + L
         return self._views(layer_idx)
 
@@ -337,7 +340,7 @@ class GemmaAttention(nn.Module):
         q = torch.empty(B * L, nh * hd, dtype=torch.bfloat16, device=dev)
         fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=past,
                             kc=st.k[self.layer_idx], vtc=st.vt[self.layer_idx], smax=st.Smax, q_heads=nh,
-                            kv_heads=nkv)
+                            kv_heads=nkv, kd=st.kd[self.layer_idx], vd=st.vd[self.layer_idx])
         ops.gemm_fused(xb, wqkv, q, fa, epi=ops.EPI_QKV_ROPE, M=B * L, bias=bqkv)
         cache._len[self.layer_idx] = past + L
         Lkv = past + L

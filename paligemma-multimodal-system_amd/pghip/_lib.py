@@ -26,7 +26,7 @@ class PgFusedArgs(C.Structure):
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
                 ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
-                ("slab_rows", C.c_int)]
+                ("slab_rows", C.c_int), ("kd", C.c_void_p), ("vd", C.c_void_p)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -38,10 +38,10 @@ SIGNATURES = {
     "pg_gemm_finalize": [vp, i32, vp, i32, i32, i32, i32, vp, i32, i32, C.POINTER(PgFusedArgs), vp],
     "pg_norm_residual": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
-                     i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp],
+                     i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp, vp, vp],
     "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
-    "pg_attn_decode": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, i32, i32, vp, i32, i32, i32, f32, i32,
-                       i32, i32, i32, vp, vp, vp, vp],
+    "pg_attn_decode": [vp, i64, vp, i64, vp, vp, i32, i32, vp, i32, i32, i32, f32, i32, i32, i32, i32, vp, vp, vp,
+                       vp],
     "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],
     "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],
     "pg_image_rank": [vp, i32, i64, vp, vp],
@@ -74,7 +74,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 def source_hash(lib=None) -> str:

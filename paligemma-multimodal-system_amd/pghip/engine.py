@@ -56,13 +56,27 @@ def rope_tables(dim: int, n_pos: int, base: float, device):
 
 
 class KVStore:
-    """Static KV cache: K [layers][B][Smax][nkv*hd] (roped), V^T [layers][B][nkv*hd][Smax], bf16."""
+    """Static KV cache: K [layers][B][Smax][nkv*hd] (roped), V^T [layers][B][nkv*hd][Smax], bf16, plus the
+    decode-order copies kd / vd [layers][B][nkv][Smax][hd] that the QKV epilogue writes beside them and the decode
+    attention kernels read (csrc/attn_common.h dec_koff / dec_voff: one contiguous KiB per load instruction)."""
 
     def __init__(self, layers: int, B: int, Smax: int, kv_dim: int, device):
         self.B, self.Smax, self.kv_dim = B, Smax, kv_dim
         self.k = torch.zeros(layers, B, Smax, kv_dim, dtype=torch.bfloat16, device=device)
         self.vt = torch.zeros(layers, B, kv_dim, Smax, dtype=torch.bfloat16, device=device)
+        self.kd = torch.zeros(layers, B * Smax * kv_dim, dtype=torch.bfloat16, device=device)
+        self.vd = torch.zeros(layers, B * Smax * kv_dim, dtype=torch.bfloat16, device=device)
         self.length = 0
+
+    def copy_prefix_from(self, old: "KVStore", n: int):
+        """Grow: the first n positions of every layer of a smaller store (canonical and decode-order copies)."""
+        nl = old.k.shape[0]
+        self.k[:nl, :, :n] = old.k[:, :, :n]
+        self.vt[:nl, :, :, :n] = old.vt[:, :, :, :n]
+        nb = -(-n // 32) * 32                     # decode-order copies hold whole 32-key blocks per (row, kv head)
+        hd_kv = self.kv_dim
+        for t_new, t_old in ((self.kd, old.kd), (self.vd, old.vd)):
+            t_new.view(-1, self.B, self.Smax, hd_kv)[:nl, :, :nb] = t_old.view(nl, old.B, old.Smax, hd_kv)[:, :, :nb]
 
 
 class PaliGemmaEngine:
@@ -254,7 +268,8 @@ class PaliGemmaEngine:
             xin = self._norm(x_resid, Lw["in_w"], part, ns, xn, T)
             # q|k|v projection + RoPE + KV-cache append in one GEMM (modeling_gemma.py:274-302)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_base=0,
-                                kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
+                                kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv,
+                                kd=cache.kd[i], vd=cache.vd[i])
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, T, fa=fa)
             ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
@@ -528,13 +543,14 @@ class PaliGemmaEngine:
             fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_a, resid_out=res_b, partials=part, nsplit=ns,
                                 norm_w=Lw["in_w"], eps=1e-6, head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"],
                                 rows_per_batch=1, slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i],
-                                vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv)
+                                vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv, kd=cache.kd[i],
+                                vd=cache.vd[i])
             ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                           scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o, part_ml=part_ml,
-                          kcap=cache.Smax)
+                          kcap=cache.Smax, kd=cache.kd[i], vd=cache.vd[i])
             fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                 akeys=SK)
@@ -579,8 +595,7 @@ class PaliGemmaEngine:
         # by one CU) costs what the combine launch does (pt-448 x16: 14.6 vs 13.6-13.8 us; profiles/r03_decode_attn_plans.txt)
         if (self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64
                 and ops.decode_plan(B, nkv, cache.Smax)[2] >= self.FUSED_MIN_ROUNDS):
-            ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
-                            cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
+            ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.kd[i], cache.vd[i],
                             B=B, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                             kcap=cache.Smax, part_o=part_o, part_ml=part_ml,
                             counters=self._zeros("d_dec_cnt", (B * nkv,), torch.int32))
@@ -589,7 +604,7 @@ class PaliGemmaEngine:
                       cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                       B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                       scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                      part_ml=part_ml, kcap=cache.Smax)
+                      part_ml=part_ml, kcap=cache.Smax, kd=cache.kd[i], vd=cache.vd[i])
         ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
 
     def _split_o(self, B: int) -> int:
@@ -633,7 +648,7 @@ class PaliGemmaEngine:
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
-                        q_heads=nh, kv_heads=nkv)
+                        q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
             if i == 0:      # the embedding rows are final: plain RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                     **rope)
@@ -646,7 +661,7 @@ class PaliGemmaEngine:
                               cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                               B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                               scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
-                              part_ml=part_ml, kcap=cache.Smax)
+                              part_ml=part_ml, kcap=cache.Smax, kd=cache.kd[i], vd=cache.vd[i])
                 fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                     head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                     akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
@@ -702,7 +717,7 @@ class PaliGemmaEngine:
             xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
-                                q_heads=nh, kv_heads=nkv)
+                                q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS, nsplit)
             self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)

@@ -194,12 +194,29 @@ def norm_residual_fp8(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, sca
 
 def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lq, Lkv, Hq, Hkv, D,
               scale, mask=None, mask_bs=0, mask_rs=0, lkv_dev=None, split_keys=0, nsplit=0, part_o=None,
-              part_ml=None, kcap=0):
+              part_ml=None, kcap=0, kd=None, vd=None):
     """q/k/vt/o are base tensors (bf16) with explicit element strides (see include/pghip.h).  kcap (decode): the
-    static cache's row capacity Smax, so each split's first K/V block is loaded before the kv length arrives."""
+    static cache's row capacity Smax, so each split's first K/V block is loaded before the kv length arrives; the
+    decode kernels then read K and V from the decode-order copies kd / vd (decode_cache_pack)."""
     _lib.call("pg_attention", _p(q), q_rs, _p(o), o_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds,
               _p(mask), mask_bs, mask_rs, B, Lq, Lkv, _p(lkv_dev), Hq, Hkv, D, float(scale), split_keys, nsplit,
-              _p(part_o), _p(part_ml), int(kcap), _s())
+              _p(part_o), _p(part_ml), int(kcap), _p(kd), _p(vd), _s())
+
+
+def decode_cache_pack(k: torch.Tensor, vt: torch.Tensor, Hkv: int):
+    """The decode-order copies (kd, vd) [B][Hkv][Smax][D] of a canonical cache (k [B][Smax][Hkv*D], vt [B][Hkv*D][Smax])
+    -- what the QKV epilogue writes beside the canonical cache (csrc/attn_common.h dec_koff / dec_voff); for tests
+    and benchmarks that build a cache by hand.  Smax % 32 == 0, D % 16 == 0."""
+    B, S, KV = k.shape
+    D = KV // Hkv
+    nb = S // 32
+    # K: key 32 blk + 8 q + 4 h + j  <->  [blk][h][D/8 chunk][row 4q + j][8]
+    kd = (k.reshape(B, nb, 4, 2, 4, Hkv, D // 8, 8).permute(0, 5, 1, 3, 6, 2, 4, 7)
+          .reshape(B, Hkv, S, D).contiguous())
+    # V: key 32 blk + 8 g + e, dim 16 t + c  <->  [blk][t][g][c][e]
+    vd = (vt.reshape(B, Hkv, D // 16, 16, nb, 4, 8).permute(0, 1, 4, 2, 5, 3, 6)
+          .reshape(B, Hkv, S, D).contiguous())
+    return kd, vd
 
 
 PF_KEYSPLIT = os.environ.get("PG_PF_KEYSPLIT", "1") != "0"
@@ -240,18 +257,18 @@ def decode_plan(B: int, Hkv: int, kcap: int, cus: int = 256):
     return nsplit, nw, nb
 
 
-def attn_decode(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale,
-                kcap, part_o, part_ml, counters, plan=None):
+def attn_decode(q, q_rs, o, o_rs, kd, vd, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale, kcap, part_o, part_ml, counters,
+                plan=None):
     """Batched decode attention with the split merge in the same launch (pg_attn_decode): o[b][hq*D + d] bf16 from
-    q (one position per row) over the static cache; part_o / part_ml / counters are workspaces (counters int32 [B*Hkv],
-    zeroed once)."""
+    q (one position per row) over the decode-order cache copies kd / vd; part_o / part_ml / counters are workspaces
+    (counters int32 [B*Hkv], zeroed once)."""
     nsplit, nw, nb = plan or decode_plan(B, Hkv, kcap)
     if part_o.numel() < B * Hkv * nsplit * 16 * D or part_ml.numel() < B * Hkv * nsplit * 16 * 2:
         raise ValueError("pghip.attn_decode: partial workspace too small")
     if counters.dtype != torch.int32 or counters.numel() < B * Hkv:
         raise ValueError("pghip.attn_decode: counters must be int32 [B*Hkv]")
-    _lib.call("pg_attn_decode", _p(q), q_rs, _p(o), o_rs, _p(k), k_bs, k_hs, k_rs, _p(vt), vt_bs, vt_hs, vt_ds, B, Lkv,
-              _p(lkv_dev), Hq, Hkv, D, float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _s())
+    _lib.call("pg_attn_decode", _p(q), q_rs, _p(o), o_rs, _p(kd), _p(vd), B, Lkv, _p(lkv_dev), Hq, Hkv, D,
+              float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _s())
 
 
 def rope_kv_write(qkv, pos, cos_t, sin_t, kc, vtc, *, T, L, Hq, Hkv, D, Smax, slot_base=0, slot_dev=None):

@@ -27,11 +27,13 @@ for name, B, L, sk in (("pt448x16", 16, 1096, 32), ("pt896x32", 32, 4168, 32),
     nsplit = ((Smax + sk - 1) // sk + 3) // 4 * 4
     po = torch.empty(B * nsplit * 16 * 256, device="cuda")
     pml = torch.empty(B * nsplit * 16 * 2, device="cuda")
+    kd, vd = ops.decode_cache_pack(kc.view(4 * B, Smax, hd), vtc.view(4 * B, hd, Smax), nkv)
+    kd, vd = kd.view(4, B, -1), vd.view(4, B, -1)
     for rep in range(6):
         i = rep % 4
         ops.attention(q, nh * hd, None, nh * hd, kc[i], Smax * hd, hd, hd, vtc[i], hd * Smax, hd * Smax, Smax,
                       B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=sk,
-                      nsplit=nsplit, part_o=po, part_ml=pml, kcap=Smax)
+                      nsplit=nsplit, part_o=po, part_ml=pml, kcap=Smax, kd=kd[i], vd=vd[i])
         torch.cuda.synchronize()
     n = B * nsplit
     buf = np.zeros((n, 4), dtype=np.uint64)

@@ -24,6 +24,8 @@ for name, B, L in (("pt448x16", 16, 1096), ("pt896x32", 32, 4168), ("pt224x1", 1
     q = (torch.randn(B, nh * hd, device="cuda")).to(torch.bfloat16)
     lkv = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
     o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
+    packed = [ops.decode_cache_pack(kc[i], vtc[i], nkv) for i in range(layers)]
+    kd, vd = [p[0] for p in packed], [p[1] for p in packed]
     dt = 256
     # the fused kernel (pg_attn_decode: attention + merge in one launch) at its default plan and neighbours
     cnt = torch.zeros(B * nkv, dtype=torch.int32, device="cuda")
@@ -38,7 +40,7 @@ for name, B, L in (("pt448x16", 16, 1096), ("pt896x32", 32, 4168), ("pt224x1", 1
         pml = torch.empty(B * nkv * plan[0] * 16 * 2, device="cuda")
 
         def layer(i, plan=plan, po=po, pml=pml):
-            ops.attn_decode(q, nh * hd, o, nh * hd, kc[i], Smax * kvd, hd, kvd, vtc[i], kvd * Smax, hd * Smax, Smax,
+            ops.attn_decode(q, nh * hd, o, nh * hd, kd[i], vd[i],
                             B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=Smax, part_o=po,
                             part_ml=pml, counters=cnt, plan=plan)
         layer(0)
@@ -74,7 +76,7 @@ for name, B, L in (("pt448x16", 16, 1096), ("pt896x32", 32, 4168), ("pt224x1", 1
         def layer(i):
             ops.attention(q, nh * hd, None, nh * hd, kc[i], Smax * kvd, hd, kvd, vtc[i], kvd * Smax, hd * Smax, Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=sk,
-                          nsplit=nsplit, part_o=po, part_ml=pml, kcap=Smax)
+                          nsplit=nsplit, part_o=po, part_ml=pml, kcap=Smax, kd=kd[i], vd=vd[i])
             ops.attn_combine(po, pml, o, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
         layer(0)
         torch.cuda.synchronize()

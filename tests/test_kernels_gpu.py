@@ -345,11 +345,12 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
         po1 = torch.empty(B * nkv * ns * 16 * dt, device="cuda")
         pml1 = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
         outs = []
+        kd, vd = ops.decode_cache_pack(kc, vtc, nkv)      # kcap > 0 reads the decode-order copies
         for kcap in (0, Smax):
             od2 = torch.empty_like(od)
             ops.attention(qd, nh * hd, od2, nh * hd, kc, Smax * kvd, hd, kvd, vtc, kvd * Smax, hd * Smax, Smax,
                           B=B, Lq=1, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, split_keys=sk,
-                          nsplit=ns, part_o=po1, part_ml=pml1, kcap=kcap)
+                          nsplit=ns, part_o=po1, part_ml=pml1, kcap=kcap, kd=kd, vd=vd)
             ops.attn_combine(po1, pml1, od2, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=ns)
             assert err(od2, ref[:, :, -1].reshape(B, nh * hd)) < 2e-2, (sk, kcap)
             outs.append(od2)
@@ -377,6 +378,7 @@ def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
     vf = vtc[:, :, :L].float().view(B, nkv, hd, L).transpose(2, 3).repeat_interleave(g, 1)
     ref = _attn_ref(q.view(B, nh, 1, hd), kf, vf, hd ** -0.5).reshape(B, nh * hd)
     cnt = torch.zeros(B * nkv, dtype=torch.int32, device="cuda")
+    kd, vd = ops.decode_cache_pack(kc, vtc, nkv)
     nblk = kcap // 32
     plans = {ops.decode_plan(B, nkv, kcap)}
     for nw in (2, 4):
@@ -390,7 +392,7 @@ def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
         pml = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
         o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
         for rep in range(2):
-            ops.attn_decode(q, nh * hd, o, nh * hd, kc, kcap * kvd, hd, kvd, vtc, kvd * kcap, hd * kcap, kcap,
+            ops.attn_decode(q, nh * hd, o, nh * hd, kd, vd,
                             B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=kcap, part_o=po,
                             part_ml=pml, counters=cnt, plan=plan)
             torch.cuda.synchronize()
@@ -694,12 +696,17 @@ def test_gemm_fused_qkv_rope_epilogue(M, L, H):
     q = torch.empty(M, nh * hd, dtype=torch.bfloat16, device="cuda")
     kc = torch.zeros_like(kc_r)
     vt = torch.zeros_like(vt_r)
+    kd = torch.zeros(B * Smax * nkv * hd, dtype=torch.bfloat16, device="cuda")
+    vd = torch.zeros_like(kd)
     fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=pos, rows_per_batch=L, slot_dev=slot, slot_base=3,
-                        kc=kc, vtc=vt, smax=Smax, q_heads=nh, kv_heads=nkv)
+                        kc=kc, vtc=vt, smax=Smax, q_heads=nh, kv_heads=nkv, kd=kd, vd=vd)
     ops.gemm_fused(x, Wp, q, fa, epi=ops.EPI_QKV_ROPE, M=M)
     assert err(q, qkv[:, :nh * hd]) < 1e-2
     assert err(kc, kc_r) < 1e-2
     assert err(vt, vt_r) < 1e-2
+    # the decode-order copies (ABI 6) hold exactly the canonical cache's bytes, permuted (csrc dec_koff / dec_voff)
+    kd_r, vd_r = ops.decode_cache_pack(kc, vt, nkv)
+    assert torch.equal(kd.view_as(kd_r), kd_r) and torch.equal(vd.view_as(vd_r), vd_r)
 
 
 @pytest.mark.parametrize("H,W,S", [(480, 640, 224), (37, 51, 224), (224, 500, 224), (1000, 224, 448),
