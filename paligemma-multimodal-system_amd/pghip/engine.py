@@ -591,8 +591,9 @@ class PaliGemmaEngine:
         nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
         # the one-launch kernel where the cache needs several rounds of waves (pt-896 x32: 34.3 vs 43.3 us per layer,
-        # attention + merge); with one or two rounds its last split's serial merge of every partial (64-152 KB read
-        # by one CU) costs what the combine launch does (pt-448 x16: 14.6 vs 13.6-13.8 us; profiles/r03_decode_attn_plans.txt)
+        # attention + merge); with one or two rounds its last split's serial merge of every partial (64 KB read by
+        # one CU) costs more than the combine launch: pt-448 x16 1.429 vs 1.412 ms/step, pt-224 x16 1.374 vs
+        # 1.350 (scripts/gpu_ab_fused.sh, interleaved, one box)
         if (self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64
                 and ops.decode_plan(B, nkv, cache.Smax)[2] >= self.FUSED_MIN_ROUNDS):
             ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.kd[i], cache.vd[i],

@@ -242,17 +242,15 @@ def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
     _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
 
 
-def decode_plan(B: int, Hkv: int, kcap: int, cus: int = 256):
-    """(nsplit, nw, nb) of pg_attn_decode for a batch of B rows over a static cache of kcap keys: about one workgroup
-    per CU (measured: pt-896 x32, 8 splits x 4 waves x 5 rounds 38.6 us per layer vs 42.4 at 16 splits x 3 rounds, two
-    workgroups per CU; scripts/tune/decode_attn_bench.py), the kcap/32 blocks of a (row, kv head) dealt round-robin
-    to its splits; 4 waves per split when every wave of one workgroup per CU gets a block, else 2; at most 16 splits,
-    the partials the last split merges in one round trip."""
+def decode_plan(B: int, Hkv: int, kcap: int):
+    """(nsplit, nw, nb) of pg_attn_decode for a batch of B rows over a static cache of kcap keys: 4 waves per split
+    and at most 8 splits per (row, kv head), the rounds following from the cache length.  The last split's workgroup
+    merges every partial alone (8 KB each), so fewer splits win while the rounds stay few: measured per layer
+    (attention + merge, profiles/r03_decode_attn_plans.txt) pt-448 x16 8 x 4 x 2 12.7 us vs 16 x 2 x 2 13.9 and
+    5 x 4 x 2 13.1; pt-896 x32 8 x 4 x 5 31.9 vs 6 x 4 x 6 30.9, 16 x 4 x 3 37.8, 16 x 2 x 5 35.4."""
     nblk = kcap // 32
-    rows = max(1, B * Hkv)
-    nw = 4 if rows * nblk >= 4 * cus else 2
-    s_max = max(1, min(16, cus // rows))
-    nsplit = max(1, min(s_max, nblk // nw))
+    nw = 4 if nblk >= 4 else 2
+    nsplit = max(1, min(8, nblk // nw))
     nb = -(-nblk // (nw * nsplit))
     return nsplit, nw, nb
 
