@@ -621,9 +621,14 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
 // across the barrier).  NST 2 / KB 64 for grids that fill the chip; a deep ring (NST 5-8) for the batch-1 grids
 // of a few dozen workgroups, whose time is otherwise one L2 round trip per block.  Images:
 //   K   : 16-key groups of [DP/8 chunks][16 keys][16 B] -> a S^T fragment read (16 keys x 32 d) is one
-//         contiguous KiB per wave-instruction (conflict-free ds_read_b128)
+//         contiguous KiB per wave-instruction (conflict-free ds_read_b128).  Image row i of group kt holds key
+//         32 (kt / 2) + 8 (i / 4) + 4 (kt % 2) + i % 4 (the source address picks it), so the S^T lanes of a
+//         32-key half hold 8 CONSECUTIVE keys 8g..8g+7 and a PV fragment of V^T is one 16-B chunk
 //   V^T : rows of 2 KB bytes, 16-B chunk XOR-swizzled through the source address by (row >> 1) & 7 (KB 64) or
-//         (row >> 2) & 3 (KB 32) -> the two ds_read_b64 of a PV fragment are conflict-free
+//         (row >> 2) & 2 (KB 32) -> the one ds_read_b128 of a PV fragment is conflict-free (16 distinct slots
+//         in each of its 16-lane groups).  The earlier key order needed two 8-B reads per fragment, which the
+//         compiler pairs into ds_read2st64_b64 (half the LDS rate, 2-way conflicts on the 32-bank modulus):
+//         the LDS, not the MFMA, bounded the kernel
 // Per block a wave does 4 x KS S^T MFMAs, an online softmax on 16 scores per lane (the rescale of O is
 // skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
 // V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row);
@@ -678,7 +683,8 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     char* vimg = kimg + KIMG;
     for (int i = wave; i < KINS; i += WAVES) {
       const int kg = i / (NCH / 4), cq = i % (NCH / 4);
-      const int ch = 4 * cq + (lane >> 4), key = 16 * kg + (lane & 15);
+      const int i16 = lane & 15;
+      const int ch = 4 * cq + (lane >> 4), key = 32 * (kg >> 1) + 8 * (i16 >> 2) + 4 * (kg & 1) + (i16 & 3);
       // chunks past D (D < DP) re-read chunk 0: the matching q dims are zero, and 0 * (finite K) = 0, whereas
       // the bytes past a head's D may be another tensor's never-written memory (NaN * 0 = NaN)
       const bf16_t* src = kbase + (long)min(kb + key, Lkv - 1) * a.k_rs + (ch * 8 < D ? ch * 8 : 0);
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     }
     for (int i = wave; i < VINS; i += WAVES) {
       const int row = KB == 64 ? 8 * i + (lane >> 3) : 16 * i + (lane >> 2);
-      const int cl = KB == 64 ? (lane & 7) ^ ((row >> 1) & 7) : (lane & 3) ^ ((row >> 2) & 3);
+      const int cl = KB == 64 ? (lane & 7) ^ ((row >> 1) & 7) : (lane & 3) ^ ((row >> 2) & 2);
       const bf16_t* src = vbase + (long)min(row, D - 1) * a.vt_ds + min(kb + 8 * cl, vkey_max);
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(vimg + i * 1024), 16, 0, 0);
     }
@@ -734,7 +740,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < RPW; ++i) sc[i][kt] = mfma16(kf, qf[i][s], sc[i][kt]);
       }
-    // lane holds S[key = kb + 16 kt + 4g + j][q = c] of each row group
+    // lane holds S[key = kb + 32 (kt / 2) + 8g + 4 (kt % 2) + j][q = c] of each row group
     bf16x8 pf[RPW][KB / 32];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
@@ -748,7 +754,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
         for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (kb + 16 * kt + 4 * g + j >= Lkv) x[4 * kt + j] = -INFINITY;
+            if (kb + 32 * (kt >> 1) + 8 * g + 4 * (kt & 1) + j >= Lkv) x[4 * kt + j] = -INFINITY;
       }
       float bm = x[0];
 #pragma unroll
@@ -768,7 +774,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
         for (int tt = 0; tt < DT; ++tt) o[i][tt] *= alpha;
       }
-      // P^T operand of the two 32-key steps; slot 8g+j <-> key 32h + 4g + j (j < 4), 32h + 16 + 4g + j - 4
+      // P^T operand of the 32-key steps; slot 8g+j <-> key 32h + 8g + j
 #pragma unroll
       for (int h = 0; h < KB / 32; ++h) {
         u32x4 pw;
@@ -786,11 +792,8 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       for (int tt = 0; tt < DT; ++tt) {
         const int row = 16 * tt + c;
         const char* vr = vimg + row * VROW;
-        const int sw = KB == 64 ? (row >> 1) & 7 : (row >> 2) & 3;
-        const int c0 = 4 * h, c1 = 4 * h + 2;                 // 16-B chunks of keys 32h + 4g.. and 32h + 16 + 4g..
-        const u32x2 v0 = *(const u32x2*)(vr + ((c0 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
-        const u32x2 v1 = *(const u32x2*)(vr + ((c1 + (g >> 1)) ^ sw) * 16 + (g & 1) * 8);
-        const bf16x8 vf = __builtin_bit_cast(bf16x8, u32x4{v0[0], v0[1], v1[0], v1[1]});
+        const int sw = KB == 64 ? (row >> 1) & 7 : (row >> 2) & 2;
+        const bf16x8 vf = *(const bf16x8*)(vr + ((4 * h + g) ^ sw) * 16);   // keys 32h + 8g .. + 7
 #pragma unroll
         for (int i = 0; i < RPW; ++i) o[i][tt] = mfma16(vf, pf[i][h], o[i][tt]);
       }
