@@ -393,15 +393,15 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     float bm = x[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    bm = max_xor16(bm);
+    bm = max_xor32(bm);
     const float mn = fmaxf(m, bm);
     const float alpha = exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { x[j] = exp2f(x[j] - mn); rs += x[j]; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = sum_xor16(rs);
+    rs = sum_xor32(rs);
     l = l * alpha + rs;
     m = mn;
 #pragma unroll
@@ -570,15 +570,15 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
     float bm = x[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    bm = max_xor16(bm);
+    bm = max_xor32(bm);
     const float mn = fmaxf(m, bm);
     const float alpha = exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { x[j] = exp2f(x[j] - mn); rs += x[j]; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = sum_xor16(rs);
+    rs = sum_xor32(rs);
     l = l * alpha + rs;
     m = mn;
     u32x4 pw;
@@ -759,15 +759,15 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       float bm = x[0];
 #pragma unroll
       for (int j = 1; j < 4 * NKT; ++j) bm = fmaxf(bm, x[j]);
-      bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-      bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+      bm = max_xor16(bm);
+      bm = max_xor32(bm);
       const float mn = fmaxf(m[i], bm);
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
       float rs = 0.f;
 #pragma unroll
       for (int j = 0; j < 4 * NKT; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = sum_xor16(rs);
+      rs = sum_xor32(rs);
       l[i] = l[i] * alpha + rs;
       m[i] = mn;
       if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O

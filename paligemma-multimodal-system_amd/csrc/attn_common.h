@@ -231,16 +231,16 @@ __device__ __forceinline__ void attn_decode_split(const AttnArgs& a, int b, int 
     float bm = x[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
-    bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-    bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+    bm = max_xor16(bm);
+    bm = max_xor32(bm);
     const float mn = fmaxf(m, bm);
     const bool none = mn == -INFINITY;          // every key of the block masked and nothing before it
     const float alpha = none ? 1.f : exp2f(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = sum_xor16(rs);
+    rs = sum_xor32(rs);
     m = mn;
     if constexpr (decltype(first)::value) {
       l = rs;
@@ -369,14 +369,14 @@ __device__ __forceinline__ void attn_decode_block32(const AttnArgs& a, int b, in
   float bm = x[0];
 #pragma unroll
   for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
-  bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  bm = max_xor16(bm);
+  bm = max_xor32(bm);
   const bool none = bm == -INFINITY;            // every key of the block masked
   float rs = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - bm); rs += x[j]; }
-  rs += __shfl_xor(rs, 16, 64);
-  rs += __shfl_xor(rs, 32, 64);
+  rs = sum_xor16(rs);
+  rs = sum_xor32(rs);
   m = bm;
   l = rs;
   u32x4 pw;
@@ -443,16 +443,16 @@ __device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int k
   float bm = x[0];
 #pragma unroll
   for (int j = 1; j < 8; ++j) bm = fmaxf(bm, x[j]);
-  bm = fmaxf(bm, __shfl_xor(bm, 16, 64));
-  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  bm = max_xor16(bm);
+  bm = max_xor32(bm);
   const float mn = fmaxf(m, bm);
   const bool none = mn == -INFINITY;          // every key so far masked
   const float alpha = none ? 1.f : exp2f(m - mn);
   float rs = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { x[j] = none ? 0.f : exp2f(x[j] - mn); rs += x[j]; }
-  rs += __shfl_xor(rs, 16, 64);
-  rs += __shfl_xor(rs, 32, 64);
+  rs = sum_xor16(rs);
+  rs = sum_xor32(rs);
   m = mn;
   if constexpr (FIRST) {                        // (o, m, l) = (0, -inf, 0): nothing to rescale
     l = rs;

@@ -19,8 +19,39 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> packed bf16 pair (RNE): one v_cvt_pk_bf16_f32 (converting each half separately costs two
+// converts plus a shift and an OR per pair)
+typedef __bf16 pg_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float pg_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(pg_f32x2_t{lo, hi}, pg_bf16x2_t));
+}
+
+// combine lane l with lane l ^ 16 / l ^ 32 in registers: gfx950's v_permlane16_swap / v_permlane32_swap hand
+// back both lanes' values (a VALU op; __shfl_xor is a ds_bpermute round trip through the LDS).  max and + are
+// commutative, so the result has the same bits as op(v, __shfl_xor(v, 16 / 32)) in every lane.
+__device__ __forceinline__ float max_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// the value of lane l ^ 32 (v_permlane32_swap moves the upper half of its first operand's lanes into the lower
+// half of the second and back: lanes 0-31 find their partner in the second result, lanes 32-63 in the first)
+__device__ __forceinline__ float xchg_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {

@@ -204,7 +204,7 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
   if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);   // bias in packed (permuted) column order
   f32x4 pr;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+  for (int j = 0; j < 4; ++j) pr[j] = xchg_xor32(v[j]);
   epi_qkv_rope4_pr(e, m, n0, v, pr);
 }
 
@@ -1205,8 +1205,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       for (int k = 0; k < 4; ++k) ss += lane % lpr + k * lpr < e.f.ss_n ? ssv[k] : 0.f;
     }
     if (SS16 && M > 2) {
-      ss += __shfl_xor(ss, 16, 64);
-      ss += __shfl_xor(ss, 32, 64);
+      ss = sum_xor16(ss);
+      ss = sum_xor32(ss);
     } else {
       const int lpr = M == 1 ? 64 : 32;
       for (int o = 1; o < lpr; o <<= 1) ss += __shfl_xor(ss, o, 64);
@@ -1250,8 +1250,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
           finish(t, n0, fin_r[t] + v, ssl);
         }
       }
-      ssl += __shfl_xor(ssl, 16, 64);
-      ssl += __shfl_xor(ssl, 32, 64);
+      ssl = sum_xor16(ssl);
+      ssl = sum_xor32(ssl);
       put_ss(ssl);
       return;
     }
@@ -1298,8 +1298,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
         finish(t, n0, v, ssl);
       }
     }
-    ssl += __shfl_xor(ssl, 16, 64);
-    ssl += __shfl_xor(ssl, 32, 64);
+    ssl = sum_xor16(ssl);
+    ssl = sum_xor32(ssl);
     put_ss(ssl);
     if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1314,7 +1314,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
       if (e.bias && n0 < e.N) v += load4_guard(e.bias, n0, e.N);
       f32x4 pr;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pr[j] = __shfl_xor(v[j], 32, 64);
+      for (int j = 0; j < 4; ++j) pr[j] = xchg_xor32(v[j]);
       epi_qkv_rope4_core(e, m, n0, v, pr, rope_cs[t], rope_sn[t], e.f.slot_base + rope_slot_raw);
     }
   } else {
