@@ -744,11 +744,13 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     bf16x8 pf[RPW][KB / 32];
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
+      // raw scores (keys past Lkv -> -inf); the scale (> 0) goes onto the max and into one packed fma per pair of
+      // scores before exp2 (v_pk_fma_f32 / v_pk_add_f32: the softmax, not the MFMA, bounds head_dim 72)
       float x[4 * NKT];
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[i][kt][j] * a.scale_log2;
+        for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[i][kt][j];
       if (kb + KB > Lkv) {
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
@@ -761,11 +763,18 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       for (int j = 1; j < 4 * NKT; ++j) bm = fmaxf(bm, x[j]);
       bm = max_xor16(bm);
       bm = max_xor32(bm);
-      const float mn = fmaxf(m[i], bm);
+      const float mn = fmaxf(m[i], bm * a.scale_log2);   // = the max of the scaled scores (scaling is monotonic)
       const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
-      float rs = 0.f;
+      const f32x2 s2 = {a.scale_log2, a.scale_log2}, n2 = {-mn, -mn};
+      f32x2 rs2 = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4 * NKT; ++j) { x[j] = __builtin_amdgcn_exp2f(x[j] - mn); rs += x[j]; }
+      for (int j = 0; j < 4 * NKT; j += 2) {
+        const f32x2 t = __builtin_elementwise_fma(f32x2{x[j], x[j + 1]}, s2, n2);
+        x[j] = __builtin_amdgcn_exp2f(t[0]);
+        x[j + 1] = __builtin_amdgcn_exp2f(t[1]);
+        rs2 += f32x2{x[j], x[j + 1]};
+      }
+      float rs = rs2[0] + rs2[1];
       rs = sum_xor16(rs);
       rs = sum_xor32(rs);
       l[i] = l[i] * alpha + rs;
