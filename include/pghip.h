@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -151,10 +151,13 @@ int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, in
  * (batch, kv head) are dealt round-robin to nsplit splits of nw (2 or 4) waves, nb rounds each (nw*nsplit <=
  * kcap/32 <= nw*nsplit*nb); the last-arriving split (one agent-scope ticket in counters[b*Hkv + kvh], left zero)
  * merges the partials and writes o[b][hq][0..D) bf16.  D = 32 or 256.  The cache must hold finite values in every
- * row below kcap (masked keys get weight 0 but their V is not zeroed). */
+ * row below kcap (masked keys get weight 0 but their V is not zeroed).  q8 (optional, ABI 7; Hkv == 1 and
+ * Hq*D/8 <= nw*64): the merging workgroup also writes the row as fp8 e4m3, q8[b*q8_ld + hq*D + d], with
+ * q8_scale[b] -- the bytes pg_quant_fp8 makes from o, so the fp8 o_proj needs no quantiser launch. */
 int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* kd, const void* vd, int B, int Lkv,
                    const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit, int nw, int nb,
-                   float* part_o, float* part_ml, int* counters, hipStream_t stream);
+                   float* part_o, float* part_ml, int* counters, void* q8, float* q8_scale, long q8_ld,
+                   hipStream_t stream);
 
 /* RoPE (gemma.py:112-151) on q in place and k; k -> cache rows, v -> transposed cache (KVCache.update
  * gemma.py:18-57 as a static in-place append). */

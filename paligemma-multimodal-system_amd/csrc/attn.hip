@@ -136,7 +136,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
 // (one wave per SIMD) a split's compute (0.9 us) never overlapped another split's loads, and pt-896 x32 ran 4.25
 // rounds of waves (54 us for 142 MB of K/V); this kernel holds 240 registers (two waves per SIMD).
 template <int DP, int DT, int NW>
-__global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs a, int nb, int* __restrict__ cnt) {
+__global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs a, int nb, int* __restrict__ cnt,
+                                                                      uint8_t* __restrict__ q8, float* __restrict__ q8s,
+                                                                      long q8_ld) {
   static_assert(NW == 2 || NW == 4, "2 or 4 waves per split");
   constexpr int KS = DP / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
@@ -248,6 +250,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        // compiler-only: the loads stay below the ticket
   // the last split's workgroup merges the S partials: one thread per (q row, 8 dims), 16 splits per round trip
   constexpr int D8 = DP / 8, MCH = 16;
+  u32x4 pk = {0u, 0u, 0u, 0u};                      // this thread's last 8 outputs (the fp8 copy below)
   for (int it = threadIdx.x; it < G * D8; it += NW * 64) {
     const int r = it / D8, d8 = it % D8;
     float M = -INFINITY, den = 0.f;
@@ -281,12 +284,35 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
       M = Mn;
     }
     const float inv = 1.0f / den;
-    u32x4 pk;
     pk[0] = pack_bf2(n0[0] * inv, n0[1] * inv);
     pk[1] = pack_bf2(n0[2] * inv, n0[3] * inv);
     pk[2] = pack_bf2(n1[0] * inv, n1[1] * inv);
     pk[3] = pack_bf2(n1[2] * inv, n1[3] * inv);
     *(u32x4*)(a.o + (long)b * a.o_rs + (long)(kvh * G + r) * DP + 8 * d8) = pk;
+  }
+  if (q8) {
+    // e4m3 copy of the row for the fp8 o_proj (host: one kv head, so this workgroup wrote the whole row, and one
+    // (q row, 8 dims) item per thread): pg_quant_fp8's bytes and scale from the same bf16 values
+    __shared__ float red[NW];
+    float amax = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) amax = fmaxf(amax, fmaxf(fabsf(bf_lo(pk[j])), fabsf(bf_hi(pk[j]))));
+    amax = wave_max(amax);
+    if (lane == 0) red[wave] = amax;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NW; ++w) amax = fmaxf(amax, red[w]);
+    const float s = amax > 0.f ? amax / 448.f : 1.f;
+    if (threadIdx.x == 0) q8s[b] = s;
+    if ((int)threadIdx.x < G * D8) {
+      const int r = threadIdx.x / D8, d8 = threadIdx.x % D8;
+      u32x2 w8;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        w8[j] = pack_fp8x4(bf_lo(pk[2 * j]) / s, bf_hi(pk[2 * j]) / s, bf_lo(pk[2 * j + 1]) / s,
+                           bf_hi(pk[2 * j + 1]) / s);
+      *(u32x2*)(q8 + b * q8_ld + (long)r * DP + 8 * d8) = w8;
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1143,8 +1169,12 @@ extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B,
 // [B * Hkv], zero before the first call (every call leaves them zero).  head_dim 32 or 256, D == head_dim.
 extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* kd, const void* vd, int B,
                               int Lkv, const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit,
-                              int nw, int nb, float* part_o, float* part_ml, int* counters, hipStream_t stream) {
+                              int nw, int nb, float* part_o, float* part_ml, int* counters, void* q8,
+                              float* q8_scale, long q8_ld, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && (D == 32 || D == 256));
+  // the fp8 copy: the merging workgroup holds the whole row (one kv head, one item per thread)
+  if (q8) PG_REQUIRE(Hkv == 1 && Hq * (D / 8) <= nw * 64 && q8_scale && q8_ld >= (long)Hq * D && q8_ld % 8 == 0 &&
+                     ((uintptr_t)q8 & 7) == 0);
   PG_REQUIRE((nw == 2 || nw == 4) && kcap % 32 == 0 && nsplit >= 1 && nw * nsplit <= kcap / 32 && nb >= 1 &&
              nsplit * nw * nb >= kcap / 32 && part_o && part_ml && counters && o && lkv_dev && kd && vd);
   PG_REQUIRE((long)B * Hkv * nsplit * 16 * D * 4 < 0x7fffffffL);
@@ -1155,13 +1185,17 @@ extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, cons
              (const bf16_t*)kd, (const bf16_t*)vd};
   const dim3 grid(nsplit, Hkv, B);
   if (D == 256 && nw == 4)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 4>), grid, dim3(256), 0, stream, a, nb, counters);
+    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 4>), grid, dim3(256), 0, stream, a, nb, counters,
+                       (uint8_t*)q8, q8_scale, q8_ld);
   else if (D == 256)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 2>), grid, dim3(128), 0, stream, a, nb, counters);
+    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 2>), grid, dim3(128), 0, stream, a, nb, counters,
+                       (uint8_t*)q8, q8_scale, q8_ld);
   else if (nw == 4)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 4>), grid, dim3(256), 0, stream, a, nb, counters);
+    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 4>), grid, dim3(256), 0, stream, a, nb, counters,
+                       (uint8_t*)q8, q8_scale, q8_ld);
   else
-    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 2>), grid, dim3(128), 0, stream, a, nb, counters);
+    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 2>), grid, dim3(128), 0, stream, a, nb, counters,
+                       (uint8_t*)q8, q8_scale, q8_ld);
   PG_LAUNCH_CHECK();
   return 0;
 }

@@ -27,6 +27,16 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(pg_f32x2_t{lo, hi}, pg_bf16x2_t));
 }
 
+// the two bf16 halves of a packed pair as floats
+__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+// e4m3 bytes of four floats already divided by their row scale (clamped to +-448, round to nearest even)
+__device__ __forceinline__ uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(a, -448.f), 448.f), fminf(fmaxf(b, -448.f), 448.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(fminf(fmaxf(c, -448.f), 448.f), fminf(fmaxf(d, -448.f), 448.f), w, true);
+  return (uint32_t)w;
+}
+
 // combine lane l with lane l ^ 16 / l ^ 32 in registers: gfx950's v_permlane16_swap / v_permlane32_swap hand
 // back both lanes' values (a VALU op; __shfl_xor is a ds_bpermute round trip through the LDS).  max and + are
 // commutative, so the result has the same bits as op(v, __shfl_xor(v, 16 / 32)) in every lane.

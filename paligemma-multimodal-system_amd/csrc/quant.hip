@@ -10,9 +10,6 @@
 // HBM-bound: 2 + 1 bytes per element.
 #include "common.h"
 
-__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
-__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
-
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __restrict__ x, int ldx, int K,
                                                              uint8_t* __restrict__ q, int ldq,
                                                              float* __restrict__ scale) {
@@ -37,15 +34,8 @@ __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const bf16_t* __res
     const u32x4 v = *(const u32x4*)(xr + k);
     u32x2 o;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float a = fminf(fmaxf(bf_lo(v[2 * j]) / s, -448.f), 448.f);
-      const float b = fminf(fmaxf(bf_hi(v[2 * j]) / s, -448.f), 448.f);
-      const float c = fminf(fmaxf(bf_lo(v[2 * j + 1]) / s, -448.f), 448.f);
-      const float d = fminf(fmaxf(bf_hi(v[2 * j + 1]) / s, -448.f), 448.f);
-      int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-      w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
-      o[j] = (uint32_t)w;
-    }
+    for (int j = 0; j < 2; ++j)
+      o[j] = pack_fp8x4(bf_lo(v[2 * j]) / s, bf_hi(v[2 * j]) / s, bf_lo(v[2 * j + 1]) / s, bf_hi(v[2 * j + 1]) / s);
     *(u32x2*)(qr + k) = o;
   }
 }

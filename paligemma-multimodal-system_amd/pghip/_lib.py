@@ -41,7 +41,7 @@ SIGNATURES = {
                      i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp, vp, vp],
     "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
     "pg_attn_decode": [vp, i64, vp, i64, vp, vp, i32, i32, vp, i32, i32, i32, f32, i32, i32, i32, i32, vp, vp, vp,
-                       vp],
+                       vp, vp, i64, vp],
     "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],
     "pg_patch_im2col": [vp, i32, i32, i32, i32, i32, vp, i32, vp],
     "pg_image_rank": [vp, i32, i64, vp, vp],
@@ -74,7 +74,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def source_hash(lib=None) -> str:

@@ -125,6 +125,9 @@ class PaliGemmaEngine:
     # B > FUSE_MAX_B: split-KV attention and its merge in one launch (pg_attn_decode; 0 = split kernel + combine)
     DECODE_FUSED_ATTN = os.environ.get("PG_DECODE_FUSED", "1") != "0"
     FUSED_MIN_ROUNDS = int(os.environ.get("PG_FUSED_MIN_ROUNDS", "3"))   # ... used from this many rounds per split on
+    # fp8 decode (> 16 rows): the one-launch attention also writes its rows as e4m3 for the fp8 o_proj (no
+    # pg_quant_fp8 launch; same bytes)
+    ATTN_FP8_OUT = os.environ.get("PG_ATTN_FP8_OUT", "1") != "0"
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -583,9 +586,11 @@ class PaliGemmaEngine:
             self.sample(logits, st, sampler, advance=True, feats=feats)
         return logits
 
-    def _decode_attn_merged(self, i, st, cache, qb, attn, part_o, part_ml, SK, nsplit):
+    def _decode_attn_merged(self, i, st, cache, qb, attn, part_o, part_ml, SK, nsplit, want_fp8=False):
         """Split-KV decode attention of layer i for B > FUSE_MAX_B rows, merged into attn bf16 [B][nh*hd]: one
-        pg_attn_decode launch (DECODE_FUSED_ATTN), else the split kernel + pg_attn_combine."""
+        pg_attn_decode launch (DECODE_FUSED_ATTN), else the split kernel + pg_attn_combine.  want_fp8: return the
+        rows also as (e4m3, row scales) when the one-launch kernel can write them (the fp8 o_proj's input, no
+        quantiser launch), else None."""
         w = self.w
         B = qb.shape[0]
         nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
@@ -594,19 +599,25 @@ class PaliGemmaEngine:
         # attention + merge); with one or two rounds its last split's serial merge of every partial (64 KB read by
         # one CU) costs more than the combine launch: pt-448 x16 1.429 vs 1.412 ms/step, pt-224 x16 1.374 vs
         # 1.350 (scripts/gpu_ab_fused.sh, interleaved, one box)
-        if (self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64
-                and ops.decode_plan(B, nkv, cache.Smax)[2] >= self.FUSED_MIN_ROUNDS):
+        plan = ops.decode_plan(B, nkv, cache.Smax)
+        if self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64 and plan[2] >= self.FUSED_MIN_ROUNDS:
+            x8 = None
+            if want_fp8 and self.ATTN_FP8_OUT and ops.attn_decode_q8_ok(nh, nkv, hd, plan[1]):
+                x8 = (self._buf(f"x8_{nh * hd}", (B, nh * hd), torch.uint8), self._buf(f"xs_{nh * hd}", (B,),
+                                                                                     torch.float32))
             ops.attn_decode(qb, nh * hd, attn, nh * hd, cache.kd[i], cache.vd[i],
                             B=B, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                             kcap=cache.Smax, part_o=part_o, part_ml=part_ml,
-                            counters=self._zeros("d_dec_cnt", (B * nkv,), torch.int32))
-            return
+                            counters=self._zeros("d_dec_cnt", (B * nkv,), torch.int32), plan=plan,
+                            q8=x8[0] if x8 else None, q8_scale=x8[1] if x8 else None)
+            return x8
         ops.attention(qb, nh * hd, None, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
                       cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                       B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                       scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
                       part_ml=part_ml, kcap=cache.Smax, kd=cache.kd[i], vd=cache.vd[i])
         ops.attn_combine(part_o, part_ml, attn, nh * hd, B=B, Hq=nh, Hkv=nkv, D=hd, nsplit=nsplit)
+        return None
 
     def _split_o(self, B: int) -> int:
         if self.tp == 1 and B <= self.FUSE_MAX_B and not os.environ.get("PG_SPLIT_O"):
@@ -720,8 +731,9 @@ class PaliGemmaEngine:
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
-            self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS, nsplit)
-            self._lin(attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
+            a8 = self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS,
+                                          nsplit, want_fp8=self._fp8_rows(B))
+            self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
             self._allreduce(part[:so])
             xin = self._norm(res, Lw["post_w"], part, so, xn, B)
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)

@@ -256,17 +256,29 @@ def decode_plan(B: int, Hkv: int, kcap: int):
 
 
 def attn_decode(q, q_rs, o, o_rs, kd, vd, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale, kcap, part_o, part_ml, counters,
-                plan=None):
+                plan=None, q8=None, q8_scale=None):
     """Batched decode attention with the split merge in the same launch (pg_attn_decode): o[b][hq*D + d] bf16 from
     q (one position per row) over the decode-order cache copies kd / vd; part_o / part_ml / counters are workspaces
-    (counters int32 [B*Hkv], zeroed once)."""
+    (counters int32 [B*Hkv], zeroed once).  q8 uint8 [B][>= Hq*D] / q8_scale f32 [B] (optional, one kv head and a
+    4-wave plan, see attn_decode_q8_ok): also the rows as fp8 e4m3, byte-identical to quant_fp8(o)."""
     nsplit, nw, nb = plan or decode_plan(B, Hkv, kcap)
+    if q8 is not None:
+        _chk(q8, torch.uint8, "q8")
+        _chk(q8_scale, torch.float32, "q8_scale")
+        if not attn_decode_q8_ok(Hq, Hkv, D, nw) or q8.shape[0] < B or q8_scale.numel() < B:
+            raise ValueError("pghip.attn_decode: fp8 row copy needs one kv head, Hq*D/8 <= 64*nw and B rows")
     if part_o.numel() < B * Hkv * nsplit * 16 * D or part_ml.numel() < B * Hkv * nsplit * 16 * 2:
         raise ValueError("pghip.attn_decode: partial workspace too small")
     if counters.dtype != torch.int32 or counters.numel() < B * Hkv:
         raise ValueError("pghip.attn_decode: counters must be int32 [B*Hkv]")
     _lib.call("pg_attn_decode", _p(q), q_rs, _p(o), o_rs, _p(kd), _p(vd), B, Lkv, _p(lkv_dev), Hq, Hkv, D,
-              float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _s())
+              float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _p(q8), _p(q8_scale),
+              q8.stride(0) if q8 is not None else 0, _s())
+
+
+def attn_decode_q8_ok(Hq: int, Hkv: int, D: int, nw: int) -> bool:
+    """Whether pg_attn_decode can also write the fp8 row copy: the merging workgroup must hold the whole row."""
+    return Hkv == 1 and Hq * (D // 8) <= 64 * nw
 
 
 def rope_kv_write(qkv, pos, cos_t, sin_t, kc, vtc, *, T, L, Hq, Hkv, D, Smax, slot_base=0, slot_dev=None):

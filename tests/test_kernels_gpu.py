@@ -366,7 +366,9 @@ def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
 def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
     """pg_attn_decode (split-KV attention + in-launch merge, B > 2) against fp32 softmax attention over the first L
     cached keys; rows past L hold finite stale values (the static cache after a longer request), every split plan
-    (2 / 4 waves, 1..16 splits, several rounds) agrees, repeated calls are bit-identical and leave the tickets zero."""
+    (2 / 4 waves, 1..16 splits, several rounds) agrees, repeated calls are bit-identical and leave the tickets zero.
+    Where the plan allows it (one kv head, 4 waves) the second call also writes the fp8 row copy, which must equal
+    pg_quant_fp8 of the bf16 output byte for byte (ABI 7)."""
     from pghip import ops
     kvd = nkv * hd
     q = rnd(B, nh * hd, seed=31)
@@ -391,15 +393,22 @@ def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
         po = torch.empty(B * nkv * ns * 16 * hd, device="cuda")
         pml = torch.empty(B * nkv * ns * 16 * 2, device="cuda")
         o = torch.empty(B, nh * hd, dtype=torch.bfloat16, device="cuda")
+        q8ok = ops.attn_decode_q8_ok(nh, nkv, hd, plan[1])
+        q8 = torch.full((B, nh * hd), 0x55, dtype=torch.uint8, device="cuda")
+        q8s = torch.zeros(B, device="cuda")
         for rep in range(2):
             ops.attn_decode(q, nh * hd, o, nh * hd, kd, vd,
                             B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=kcap, part_o=po,
-                            part_ml=pml, counters=cnt, plan=plan)
+                            part_ml=pml, counters=cnt, plan=plan, q8=q8 if rep and q8ok else None,
+                            q8_scale=q8s if rep and q8ok else None)
             torch.cuda.synchronize()
             assert int(cnt.abs().sum()) == 0, plan
             if rep == 0:
                 first = o.clone()
         assert torch.equal(first, o), plan
+        if q8ok:
+            r8, rs = ops.quant_fp8(o)
+            assert torch.equal(q8, r8) and torch.equal(q8s, rs), plan
         assert err(o, ref) < 2e-2, plan
         outs[plan] = o
     base = next(iter(outs.values()))
