@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 8: pg_allreduce_xgmi_slabs; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -243,6 +243,11 @@ int pg_xgmi_ipc_close(void* p);
  * can be captured into a hipGraph; every rank must issue the same sequence of calls. */
 int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
                       unsigned* epochs, int* err, hipStream_t stream);
+/* (ABI 8) The same SUM where each rank contributes the sum of its nslab (1..64) split-K slabs
+ * data[s * slab_stride + i], s = 0..nslab-1 in order (slab_stride >= n, a multiple of 4): the result is written
+ * to data[0, n).  A row-parallel o_proj / down_proj then moves one slab over xGMI, with no slab-sum launch. */
+int pg_allreduce_xgmi_slabs(float* data, long n, int nslab, long slab_stride, int rank, int world,
+                            void* const* peers, long cap, unsigned* epochs, int* err, hipStream_t stream);
 /* All-gather in rank order over the same exchange: out[r*n + i] = rank r's in[i] (the vocabulary-parallel
  * lm_head logits; replaces the zero-padded SUM that moved W x the bytes).  in != out, both
  * 16-byte aligned; otherwise as pg_allreduce_xgmi, whose buffer and epochs it shares (calls may interleave). */

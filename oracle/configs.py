@@ -89,7 +89,17 @@ TINY = {
     },
 }
 
-CONFIGS = {"pt-224": PT_224, "mix-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY}  # mix = pt shapes
+# Toy config for tensor parallelism up to 8 ranks (BASELINE configs[4] runs Gemma at TP=8): 8 q heads : 1 kv head
+# (one q head per rank at TP=8, as the real model), head_dim 128 and hidden 1024 = 8 x 128 (the reference's o_proj
+# is hidden -> hidden, modeling_gemma.py:259; every rank's q|k|v and o slices stay fragment-packable and fp8-able),
+# intermediate 640 (80 per rank at TP=8, zero-padded to the GEMM K step), vocab 304 (38 rows per rank at TP=8,
+# padded to 48).  The vision tower is TINY's, projected to 1024.
+TINY8 = copy.deepcopy(TINY)
+TINY8.update(hidden_size=1024, projection_dim=1024)
+TINY8["text_config"].update(hidden_size=1024, intermediate_size=640, num_attention_heads=8, head_dim=128,
+                            vocab_size=304)
+
+CONFIGS = {"pt-224": PT_224, "mix-224": PT_224, "pt-448": PT_448, "pt-896": PT_896, "tiny": TINY, "tiny8": TINY8}  # mix = pt shapes
 
 
 def num_image_tokens(cfg: dict) -> int:

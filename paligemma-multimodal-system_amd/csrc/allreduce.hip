@@ -43,9 +43,10 @@ struct XgPeers {
 };
 
 template <int W, bool GATHER>
-__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(const float* __restrict__ data, long n, int rank,
-                                                             XgPeers peers, long cap, unsigned* __restrict__ epochs,
-                                                             int* __restrict__ err, float* __restrict__ out) {
+__global__ __launch_bounds__(256) void allreduce_xgmi_kernel(const float* __restrict__ data, long n, int nslab,
+                                                             long slab_stride, int rank, XgPeers peers, long cap,
+                                                             unsigned* __restrict__ epochs, int* __restrict__ err,
+                                                             float* __restrict__ out) {
   const int wg = blockIdx.x, tid = threadIdx.x;
   const unsigned e = epochs[wg] + 1u;
   __syncthreads();
@@ -53,11 +54,13 @@ __global__ __launch_bounds__(256) void allreduce_xgmi_kernel(const float* __rest
   const int set = (int)(e & 1u);
   constexpr long STRIDE = (long)PG_XG_MAXWG * PG_XG_CHUNK;
 
-  // 1. push this rank's chunks into slot `rank` of every peer (and of itself)
+  // 1. push this rank's chunks into slot `rank` of every peer (and of itself); with nslab > 1 this rank's
+  //    contribution is the sum of its split-K slabs data[s * slab_stride + i], s = 0..nslab-1, in slab order
   for (long c0 = (long)wg * PG_XG_CHUNK; c0 < n; c0 += STRIDE) {
     const long c1 = c0 + PG_XG_CHUNK < n ? c0 + PG_XG_CHUNK : n;
     for (long i = c0 + 4 * tid; i < c1; i += 1024) {
-      const f32x4 v = *(const f32x4*)(data + i);
+      f32x4 v = *(const f32x4*)(data + i);
+      for (int s = 1; s < nslab; ++s) v += *(const f32x4*)(data + (long)s * slab_stride + i);
 #pragma unroll
       for (int p = 0; p < W; ++p) {
         float* dst = (float*)((char*)peers.p[p] + PG_XG_FLAG_BYTES) + ((long)set * W + rank) * cap + i;
@@ -150,9 +153,10 @@ extern "C" int pg_xgmi_ipc_open(const void* handle64, void** out) {
 
 extern "C" int pg_xgmi_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
-static int xgmi_launch(const float* data, long n, float* out, bool gather, int rank, int world, void* const* peers,
-                       long cap, unsigned* epochs, int* err, hipStream_t stream) {
+static int xgmi_launch(const float* data, long n, int nslab, long slab_stride, float* out, bool gather, int rank,
+                       int world, void* const* peers, long cap, unsigned* epochs, int* err, hipStream_t stream) {
   PG_REQUIRE(data != nullptr && out != nullptr && peers != nullptr && epochs != nullptr && err != nullptr);
+  PG_REQUIRE(nslab >= 1 && nslab <= 64 && (nslab == 1 || (slab_stride >= n && slab_stride % 4 == 0)));
   PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && rank >= 0 && rank < world);
   PG_REQUIRE(n > 0 && n % 4 == 0 && n <= cap && cap % 4 == 0 && ((uintptr_t)data & 15) == 0 &&
              ((uintptr_t)out & 15) == 0);
@@ -166,10 +170,10 @@ static int xgmi_launch(const float* data, long n, float* out, bool gather, int r
   case WW:                                                                                                     \
     if (gather)                                                                                                \
       hipLaunchKernelGGL((allreduce_xgmi_kernel<WW, true>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n,  \
-                         rank, pp, cap, epochs, err, out);                                                     \
+                         nslab, slab_stride, rank, pp, cap, epochs, err, out);                                                     \
     else                                                                                                       \
       hipLaunchKernelGGL((allreduce_xgmi_kernel<WW, false>), dim3(PG_XG_MAXWG), dim3(256), 0, stream, data, n, \
-                         rank, pp, cap, epochs, err, out);                                                     \
+                         nslab, slab_stride, rank, pp, cap, epochs, err, out);                                                     \
     break;
   switch (world) {
     PG_XG_CASE(1)
@@ -192,7 +196,15 @@ static int xgmi_launch(const float* data, long n, float* out, bool gather, int r
 // n % 4 == 0, n <= cap, data 16-B aligned.  Every rank must issue the same sequence of calls.
 extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
                                  unsigned* epochs, int* err, hipStream_t stream) {
-  return xgmi_launch(data, n, data, false, rank, world, peers, cap, epochs, err, stream);
+  return xgmi_launch(data, n, 1, 0, data, false, rank, world, peers, cap, epochs, err, stream);
+}
+
+// The same SUM of this rank's nslab split-K slabs data[s * slab_stride + i] (s in order) over the ranks, written to
+// data[0, n) (slab 0): a row-parallel linear's partial slabs are summed locally on the way into the exchange, so
+// each rank moves n floats instead of nslab * n and no slab-sum launch precedes the exchange.
+extern "C" int pg_allreduce_xgmi_slabs(float* data, long n, int nslab, long slab_stride, int rank, int world,
+                                       void* const* peers, long cap, unsigned* epochs, int* err, hipStream_t stream) {
+  return xgmi_launch(data, n, nslab, slab_stride, data, false, rank, world, peers, cap, epochs, err, stream);
 }
 
 // out[r * n + i] = rank r's in[i] for every rank r (all-gather in rank order); in / out 16-B aligned, not
@@ -200,5 +212,5 @@ extern "C" int pg_allreduce_xgmi(float* data, long n, int rank, int world, void*
 extern "C" int pg_allgather_xgmi(const float* in, long n, float* out, int rank, int world, void* const* peers,
                                  long cap, unsigned* epochs, int* err, hipStream_t stream) {
   PG_REQUIRE(in != out);
-  return xgmi_launch(in, n, out, true, rank, world, peers, cap, epochs, err, stream);
+  return xgmi_launch(in, n, 1, 0, out, true, rank, world, peers, cap, epochs, err, stream);
 }

@@ -58,7 +58,7 @@ class KVCache:
         if st is not None and (st.B != B or st.kv_dim != kv_heads * head_dim):
             raise ValueError("KVCache: batch / kv geometry changed inside one cache")
         if st is None:
-            self._store = KVStore(layers, B, _rup(max(need, 64), 64), kv_heads * head_dim, device)
+            self._store = KVStore(layers, B, _rup(max(need, 64), 64), kv_heads * head_dim, device, kv_heads=kv_heads)
             self._len = [0] * layers
             self.layers = layers
             self._kv_heads, self._head_dim = kv_heads, head_dim
@@ -66,7 +66,7 @@ class KVCache:
         if need > st.Smax or layers > st.k.shape[0]:
             nl = max(layers, st.k.shape[0])
             new = KVStore(nl, B, _rup(max(need, 2 * st.Smax if need > st.Smax else st.Smax), 64), st.kv_dim,
-                          st.k.device)
+                          st.k.device, kv_heads=st.kv_heads)
             n = max(self._len) if self._len else 0
             new.copy_prefix_from(st, n)
             self._store = new
@@ -96,9 +96,12 @@ class KVCache:
         st.vt[layer_idx, :, :, cur:cur + L] = value_states.transpose(1, 2).reshape(B, L, nkv * hd).transpose(1, 2).to(
             st.vt.dtype)
         if hd % 16 == 0:                          # the decode-order copies the engine's decode kernels read
-            kd, vd = ops.decode_cache_pack(st.k[layer_idx], st.vt[layer_idx], nkv)
-            st.kd[layer_idx].copy_(kd.reshape(-1))
-            st.vd[layer_idx].copy_(vd.reshape(-1))
+            # repack only the 32-key blocks holding the appended positions [cur, cur + L) (the layout is
+            # block-local, attn_common.h dec_koff / dec_voff), not the whole cache on every call
+            b0, b1 = cur // 32 * 32, _rup(cur + L, 32)
+            kd, vd = ops.decode_cache_pack(st.k[layer_idx, :, b0:b1], st.vt[layer_idx, :, :, b0:b1], nkv)
+            st.kd[layer_idx].view(B, nkv, st.Smax, hd)[:, :, b0:b1] = kd
+            st.vd[layer_idx].view(B, nkv, st.Smax, hd)[:, :, b0:b1] = vd
         self._len[layer_idx] = cur + L
         return self._views(layer_idx)
 

@@ -63,6 +63,7 @@ SIGNATURES = {
     "pg_xgmi_ipc_open": [C.c_char_p, C.POINTER(C.c_void_p)],
     "pg_xgmi_ipc_close": [vp],
     "pg_allreduce_xgmi": [vp, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
+    "pg_allreduce_xgmi_slabs": [vp, i64, i32, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
     "pg_allgather_xgmi": [vp, i64, vp, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
 }
 
@@ -74,7 +75,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 def source_hash(lib=None) -> str:

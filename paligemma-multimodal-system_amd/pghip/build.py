@@ -13,7 +13,9 @@ read back with pg_source_hash / library_hash()), so a prebuilt library that
 does not match the tree next to it is rebuilt here and refused at load time
 (_lib.load(check=True)).  Objects live in a directory named after the hash of
 the compile configuration, so a change of arch or flags never relinks objects
-built for another target.
+built for another target, and each object's file name carries the sha256 of its
+own source text + every csrc header + that configuration (_obj_key): an object is
+reused only when it was compiled from exactly these bytes, whatever the mtimes say.
 """
 from __future__ import annotations
 
@@ -82,12 +84,22 @@ def _stale(defines=()) -> bool:
     return library_hash() != source_hash(defines)
 
 
-def _compile(src: str, obj_dir: str, defines=()) -> str:
-    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj]
+def _obj_key(src: str, defines=()) -> str:
+    """Content key of one object: its source, every csrc header it may include, and the compile configuration."""
+    h = hashlib.sha256()
+    for p in [src] + sorted(glob.glob(os.path.join(CSRC, "*.h"))):
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read() + b"\0")
+    h.update(" ".join([_config(), *defines]).encode())
+    return h.hexdigest()[:20]
+
+
+def _compile(src: str, obj: str, defines=()) -> str:
+    cmd = [HIPCC, *FLAGS, *[f"-D{d}" for d in defines], "-c", src, "-o", obj + ".tmp"]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr}")
+    os.replace(obj + ".tmp", obj)
     return obj
 
 
@@ -100,19 +112,21 @@ def build(force: bool = False, verbose: bool = True, out: str = LIB, defines=())
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
-    # incremental: a source is recompiled when it, or any csrc header, is newer than its object (gemm.hip alone
-    # takes minutes; include/pghip.h is the C-ABI declaration, included by no source).  misc.hip carries the
-    # source hash and is always recompiled.
-    hdr = max([os.path.getmtime(p) for p in glob.glob(os.path.join(CSRC, "*.h"))] or [0.0])
+    # incremental by content: an object is reused only if its file name carries the content key of exactly this
+    # source + headers + configuration (gemm.hip alone takes minutes).  misc.hip carries the source hash and is
+    # always recompiled.
     shash = source_hash(defines)
     hash_def = f'PG_SOURCE_HASH="{shash}"'
 
     def obj_for(src):
-        obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-        if os.path.basename(src) == "misc.hip":
-            return _compile(src, obj_dir, (*defines, hash_def))
-        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr):
-            return _compile(src, obj_dir, defines)
+        base = os.path.basename(src)
+        if base == "misc.hip":
+            return _compile(src, os.path.join(obj_dir, base + ".o"), (*defines, hash_def))
+        obj = os.path.join(obj_dir, f"{base}.{_obj_key(src, defines)}.o")
+        if force or not os.path.exists(obj):
+            for old in glob.glob(os.path.join(obj_dir, base + ".*.o")):     # objects of other source text
+                os.remove(old)
+            return _compile(src, obj, defines)
         return obj
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(obj_for, srcs))

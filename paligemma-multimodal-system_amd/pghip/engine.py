@@ -60,8 +60,10 @@ class KVStore:
     decode-order copies kd / vd [layers][B][nkv][Smax][hd] that the QKV epilogue writes beside them and the decode
     attention kernels read (csrc/attn_common.h dec_koff / dec_voff: one contiguous KiB per load instruction)."""
 
-    def __init__(self, layers: int, B: int, Smax: int, kv_dim: int, device):
-        self.B, self.Smax, self.kv_dim = B, Smax, kv_dim
+    def __init__(self, layers: int, B: int, Smax: int, kv_dim: int, device, kv_heads: int = 1):
+        if kv_dim % kv_heads:
+            raise ValueError(f"kv_dim {kv_dim} does not split into {kv_heads} kv heads")
+        self.B, self.Smax, self.kv_dim, self.kv_heads = B, Smax, kv_dim, kv_heads
         self.k = torch.zeros(layers, B, Smax, kv_dim, dtype=torch.bfloat16, device=device)
         self.vt = torch.zeros(layers, B, kv_dim, Smax, dtype=torch.bfloat16, device=device)
         self.kd = torch.zeros(layers, B * Smax * kv_dim, dtype=torch.bfloat16, device=device)
@@ -73,10 +75,12 @@ class KVStore:
         nl = old.k.shape[0]
         self.k[:nl, :, :n] = old.k[:, :, :n]
         self.vt[:nl, :, :, :n] = old.vt[:, :, :, :n]
+        if (old.B, old.kv_dim, old.kv_heads) != (self.B, self.kv_dim, self.kv_heads):
+            raise ValueError("copy_prefix_from: the stores differ in batch or kv-head layout")
         nb = -(-n // 32) * 32                     # decode-order copies hold whole 32-key blocks per (row, kv head)
-        hd_kv = self.kv_dim
-        for t_new, t_old in ((self.kd, old.kd), (self.vd, old.vd)):
-            t_new.view(-1, self.B, self.Smax, hd_kv)[:nl, :, :nb] = t_old.view(nl, old.B, old.Smax, hd_kv)[:, :, :nb]
+        hk, hd = self.kv_heads, self.kv_dim // self.kv_heads
+        for t_new, t_old in ((self.kd, old.kd), (self.vd, old.vd)):   # [layers][B][Hkv][Smax][hd] (dec_koff / voff)
+            t_new.view(-1, self.B, hk, self.Smax, hd)[:nl, :, :, :nb] = t_old.view(nl, old.B, hk, old.Smax, hd)[:, :, :, :nb]
 
 
 class PaliGemmaEngine:
@@ -143,6 +147,7 @@ class PaliGemmaEngine:
         self.split_down = self.DECODE_SPLIT_DOWN if self.tp == 1 else max(1, self.DECODE_SPLIT_DOWN // self.tp)
         if os.environ.get("PG_SPLIT_DOWN"):
             self.split_down = int(os.environ["PG_SPLIT_DOWN"])
+        self._validate_splits()
         self.device = torch.device(device)
         self.image_token_id = cfg.get("image_token_index", 256000)
         pad = cfg.get("pad_token_id")
@@ -154,6 +159,21 @@ class PaliGemmaEngine:
         self.graphs = {}
 
     # ------------------------------------------------------------------ helpers
+    def _validate_splits(self):
+        """Refuse split-K settings (tuning knobs included) that a kernel would reject at launch time, before any
+        launch: the decode o / down GEMVs finalise in-kernel (PG_EPI_F32_FIN) with at most 8 splits."""
+        w = self.w
+        if not hasattr(w, "heads"):                     # vision-only pack (modeling_siglip.SiglipVisionModel)
+            return
+        checks = [("o_proj (PG_SPLIT_O)", self.split_o, w.heads * w.head_dim, 8),
+                  ("o_proj at batch <= 2", self.DECODE_SPLIT_O_SMALL, w.heads * w.head_dim, 8),
+                  ("down_proj (PG_SPLIT_DOWN)", self.split_down, w.inter, 8)]
+        if self.TILE_M1:    # (a model too narrow for this split just skips the row-tile path, _tile_m1)
+            checks.append(("batch-1 prefill down_proj (PG_M1_DOWN)", self.TILE_M1_SPLIT["down"], 64 * 64, 64))
+        for what, ks, K, hi in checks:          # (a split past K's 64-wide chunks just computes a zero slab)
+            if not 1 <= ks <= hi:
+                raise ValueError(f"split-K {ks} for {what}: needs 1 <= split <= {hi} (K = {K})")
+
     def _buf(self, name, shape, dtype):
         t = self._ws.get(name)
         n = math.prod(shape)
@@ -171,7 +191,7 @@ class PaliGemmaEngine:
 
     def new_cache(self, B: int, Smax: int) -> KVStore:
         w = self.w
-        return KVStore(w.t_layers, B, _rup(Smax, 64), w.kv_heads * w.head_dim, self.device)
+        return KVStore(w.t_layers, B, _rup(Smax, 64), w.kv_heads * w.head_dim, self.device, kv_heads=w.kv_heads)
 
     # ------------------------------------------------------------------ vision tower
     def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False, taps: Optional[list] = None,
@@ -329,7 +349,9 @@ class PaliGemmaEngine:
         if (not self.TILE_M1 or self.fp8 or self.tp != 1 or not 256 <= M <= 288
                 or M < self.PREFILL_ROWMAJOR_MIN_M):
             return 0
-        return self.TILE_M1_SPLIT.get(name, 0)
+        ks = self.TILE_M1_SPLIT.get(name, 0)
+        K = self.w.inter if name == "down" else self.w.hidden
+        return ks if ks * 64 <= K else 0
 
     def _lin(self, x: torch.Tensor, Lw: dict, name: str, out: torch.Tensor, epi: int, M: int, ksplit: int = 1,
              fa=None):
@@ -424,9 +446,14 @@ class PaliGemmaEngine:
         ops.norm_residual(resid, norm_w, mode=ops.NORM_RMS, partials=part, nsplit=nsplit, out=xn)
         return xn
 
-    def _allreduce(self, t: torch.Tensor):
-        if self.tp > 1:
-            self.comm.all_reduce(t)
+    def _allreduce_slabs(self, part: torch.Tensor, ns: int) -> int:
+        """Complete a row-parallel linear's partial sums: one rank keeps its ns split-K slabs (the next norm adds
+        them); under TP the rank's slabs are summed into slab 0 on the way into ONE all-reduce of [rows][H] fp32
+        (xGMI: inside the exchange kernel; RCCL / gloo: a slab-sum launch first).  Returns the slab count the
+        next norm must add."""
+        if self.tp == 1:
+            return ns
+        return self.comm.all_reduce_slabs(part[:ns], ns)
 
     def _row_parallel(self, x: torch.Tensor, Lw: dict, name: str, part: torch.Tensor, T: int, ks: int) -> int:
         """A row-parallel prefill linear (o_proj / down_proj) into fp32 partial slabs; returns how many slabs the
@@ -440,10 +467,7 @@ class PaliGemmaEngine:
         C = T // self.AR_CHUNK_ROWS if T >= 2 * self.AR_CHUNK_ROWS else 1
         if C <= 1:
             self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
-            if ks > 1:
-                ops.slab_sum(part[:ks], part[0])
-            self.comm.all_reduce(part[0])
-            return 1
+            return self.comm.all_reduce_slabs(part[:ks], ks)
         bounds = [T * c // C for c in range(C + 1)]
         works = []
         for r0, r1 in zip(bounds[:-1], bounds[1:]):
@@ -558,13 +582,12 @@ class PaliGemmaEngine:
                                 head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                 akeys=SK)
             ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32 | w.wflag, M=B, ksplit=so)
-            self._allreduce(part[:so])
-            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=so,
+            n_o = self._allreduce_slabs(part, so)
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res_b, resid_out=res_a, partials=part, nsplit=n_o,
                                 norm_w=Lw["post_w"], eps=1e-6)
             ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
             ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=sd)
-            self._allreduce(part[:sd])
-            ns = sd
+            ns = self._allreduce_slabs(part, sd)
         ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
         if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
             # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
@@ -734,12 +757,11 @@ class PaliGemmaEngine:
             a8 = self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS,
                                           nsplit, want_fp8=self._fp8_rows(B))
             self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
-            self._allreduce(part[:so])
-            xin = self._norm(res, Lw["post_w"], part, so, xn, B)
+            n_o = self._allreduce_slabs(part, so)
+            xin = self._norm(res, Lw["post_w"], part, n_o, xn, B)
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
             self._lin(h, Lw, "down", part, ops.EPI_F32, B, ksplit=sd)
-            self._allreduce(part[:sd])
-            ns = sd
+            ns = self._allreduce_slabs(part, sd)
         return ns
 
     def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool,

@@ -50,6 +50,16 @@ class TPComm:
     def all_reduce(self, t: torch.Tensor):
         self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
 
+    def all_reduce_slabs(self, part: torch.Tensor, ns: int) -> int:
+        """SUM over the ranks of this rank's ns split-K slabs part[:ns] (contiguous [S][rows][H]), written to part[0]:
+        the slabs are summed locally first (ops.slab_sum, fixed slab order), so one slab crosses the links.
+        Returns 1, the slab count the next norm must add."""
+        if ns > 1:
+            from . import ops
+            ops.slab_sum(part[:ns], part[0])
+        self.all_reduce(part[0])
+        return 1
+
     def all_reduce_async(self, t: torch.Tensor):
         """SUM all-reduce that may run concurrently with later work on the current stream; call .wait() on the
         result before the stream reads t."""
@@ -129,6 +139,17 @@ class XgmiComm(TPComm):
         else:
             self._refuse_in_capture("all-reduce", t)
             super().all_reduce(t)
+
+    def all_reduce_slabs(self, part: torch.Tensor, ns: int) -> int:
+        """As TPComm.all_reduce_slabs, with the slab sum done inside the exchange kernel (pg_allreduce_xgmi_slabs:
+        the same slab order, one launch)."""
+        t = part[0]
+        if ns > 1 and self._ok(t) and part.is_contiguous():
+            self._lib.call("pg_allreduce_xgmi_slabs", t.data_ptr(), t.numel(), ns, part.stride(0), self.rank,
+                           self.world, self._peers, self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+            return 1
+        return super().all_reduce_slabs(part, ns)
 
     def all_reduce_async(self, t: torch.Tensor):
         if not self._ok(t):

@@ -15,7 +15,7 @@ Weights: oracle/synth.py's name-seeded bf16-exact synthetic tensors, loaded
 with the reference's own ``load_state_dict(strict=False)`` + ``tie_weights``
 (utils.py:33-36).
 
-Usage:  python tests/golden/make_golden.py [tiny] [pt224] [topp] [pt448] [pt896] [pt224wc]
+Usage:  python tests/golden/make_golden.py [tiny] [tiny8] [pt224] [topp] [pt448] [pt896] [pt224wc]
 """
 from __future__ import annotations
 
@@ -149,17 +149,19 @@ def capture_modules(model, n_text_layers):
     return store, hs
 
 
-def make_tiny(mp, inference, proc):
-    cfg = configs.TINY
+def make_tiny(mp, inference, proc, name="tiny", batches=(1, 2)):
+    """tiny.npz (TINY, B = 1 and 2) or tiny8.npz (TINY8, the tensor-parallel toy: B = 1, 2 and 8, the last one
+    giving every rank of a TP=8 run one image of the data-parallel vision tower)."""
+    cfg = configs.CONFIGS[name]
     model = build_reference_model(mp, cfg)
     n = configs.num_image_tokens(cfg)
     size = cfg["vision_config"]["image_size"]
     out = {}
-    for B in (1, 2):
+    for B in batches:
         imgs = synthetic_images(B, size)
         pv = pixel_values_via_reference(proc, imgs)
         ids = np.array([[cfg["image_token_index"]] * n + TINY_PROMPT_IDS] * B, dtype=np.int64)
-        if B == 2:
+        if B >= 2:
             ids[1, n + 3] = 0                                             # a pad token inside row 1
         mask = np.ones_like(ids)
         store, hs = capture_modules(model, cfg["text_config"]["num_hidden_layers"])
@@ -183,8 +185,8 @@ def make_tiny(mp, inference, proc):
     gen, logits = run_test_inference(inference, model, ids, out["b1_pixel_values"], 12)
     out["greedy_ids"] = np.array(gen, dtype=np.int64)
     out["greedy_logits"] = np.stack(logits, 0)[:, 0]
-    np.savez_compressed(os.path.join(HERE, "tiny.npz"), **out)
-    print("tiny: greedy", gen)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+    print(f"{name}: greedy", gen)
 
 
 def make_pt224(mp, inference, proc, steps=16):
@@ -371,6 +373,8 @@ if __name__ == "__main__":
     torch.manual_seed(0)
     if "tiny" in which:
         make_tiny(mp, inference, proc)
+    if "tiny8" in which:          # tensor parallelism to 8 ranks (BASELINE configs[4]'s TP=8 split)
+        make_tiny(mp, inference, proc, "tiny8", (1, 2, 8))
     if "topp" in which:
         make_topp(inference)
     if "pt224" in which:

@@ -171,3 +171,43 @@ def test_test_inference_prints_prompt_and_tokens(model, golden, tmp_path):
         inference.test_inference(model, Proc(), "cuda", "P:", str(img), 12, 0.8, 0.9, False)
     line = buf.getvalue().strip().splitlines()[-1]
     assert line == "P:|" + ",".join(str(i) for i in g["greedy_ids"].tolist()) + "|"
+
+
+def test_module_loop_grows_cache_past_initial_capacity(model, golden, W):
+    """The reference's token loop through model(...) for 200 tokens (inference.py:45-82; launch_inference.sh:6 asks
+    for 1000): the drop-in's prefill allocates L + 128 cache slots (rounded to 64: 192 here), so the decode steps past
+    it grow the static store by copy (KVCache._ensure -> KVStore.copy_prefix_from, canonical and decode-order
+    copies).  Teacher-forced with the oracle's own free-running ids, every step's last-position logits must match the
+    oracle's (< 3e-2 scaled) before and after the growth, and the grown cache must hold every position."""
+    from modeling_gemma import KVCache
+    g = golden("tiny")
+    ids0, px = g["b1_input_ids"], g["b1_pixel_values"]
+    steps = 200
+    orc = O.PaliGemmaOracle(ocfg.TINY, W, recompute_vision=False)
+    ref_ids, ref_logits = O.generate(orc, ids0, px, np.ones_like(ids0), steps, stop_token=None, record_logits=True)
+    input_ids = torch.from_numpy(ids0).cuda()
+    pixel_values = torch.from_numpy(px).cuda()
+    attention_mask = torch.ones_like(input_ids)
+    kv_cache = KVCache()
+    worst, smax = [], []
+    with torch.no_grad():
+        for t in range(steps):
+            out = model(input_ids=input_ids, pixel_values=pixel_values, attention_mask=attention_mask,
+                        kv_cache=kv_cache)
+            kv_cache = out["kv_cache"]
+            smax.append(kv_cache._store.Smax)
+            worst.append(err(out["logits"][:, -1, :], ref_logits[t]))
+            input_ids = torch.tensor([[ref_ids[t]]], device="cuda")
+            attention_mask = torch.cat([attention_mask, torch.ones((1, 1), device="cuda")], dim=-1)
+    L = ids0.shape[1]
+    assert smax[0] < L + steps <= smax[-1], (smax[0], smax[-1])      # the store grew during the loop
+    assert max(worst) < TOL, (max(worst), int(np.argmax(worst)))
+    assert kv_cache.num_items() == L + steps - 1
+    # the grown cache holds the prefill positions unchanged (same keys as a fresh prefill's)
+    k_all = kv_cache.k_cache[0]
+    assert k_all.shape[2] == L + steps - 1
+    fresh = KVCache()
+    with torch.no_grad():
+        model(input_ids=torch.from_numpy(ids0).cuda(), pixel_values=pixel_values,
+              attention_mask=torch.ones_like(torch.from_numpy(ids0)).cuda(), kv_cache=fresh)
+    assert torch.equal(k_all[:, :, :L], fresh.k_cache[0][:, :, :L])

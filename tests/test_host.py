@@ -55,7 +55,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.pg_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_library_matches_source_tree():
@@ -255,3 +255,47 @@ def test_load_hf_model_remaps_reports_and_drops(tmp_path):
     assert any(k.startswith("vision_tower.model.") for k in rep.missing) and len(rep.unexpected) > 0
     with pytest.raises(KeyError):
         load_hf_model(str(d), "cpu", strict=True)
+
+
+@pytest.mark.parametrize("nkv", [1, 2])
+def test_kvcache_grow_and_partial_repack_keep_decode_order_copies(nkv):
+    """modeling_gemma.KVCache on CPU tensors: appends of 40 then 1-token steps past the first capacity (64 -> grown),
+    with nkv kv heads.  The canonical K / V^T views equal the appended states, and the decode-order copies kd / vd that
+    update() repacks block by block (only the 32-key blocks it touched) and that KVStore.copy_prefix_from carries over
+    equal ops.decode_cache_pack of the whole canonical cache, head by head."""
+    from modeling_gemma import KVCache
+    from pghip import ops
+    torch.manual_seed(0)
+    B, hd, layers = 2, 32, 2
+    kv = KVCache()
+    ks, vs = [[] for _ in range(layers)], [[] for _ in range(layers)]
+    for L in [40] + [1] * 50:
+        for i in range(layers):
+            k = torch.randn(B, nkv, L, hd).bfloat16()
+            v = torch.randn(B, nkv, L, hd).bfloat16()
+            ks[i].append(k), vs[i].append(v)
+            kv.update(k, v, i)
+    st = kv._store
+    n = kv.num_items()
+    assert n == 90 and st.Smax >= 128
+    for i in range(layers):
+        K, V = kv.k_cache[i], kv.v_cache[i]
+        assert torch.equal(K, torch.cat(ks[i], 2)) and torch.equal(V, torch.cat(vs[i], 2))
+        kd, vd = ops.decode_cache_pack(st.k[i], st.vt[i], nkv)
+        nb = -(-n // 32) * 32
+        got_k = st.kd[i].view(B, nkv, st.Smax, hd)[:, :, :nb]
+        got_v = st.vd[i].view(B, nkv, st.Smax, hd)[:, :, :nb]
+        assert torch.equal(got_k, kd[:, :, :nb]) and torch.equal(got_v, vd[:, :, :nb])
+
+
+def test_engine_refuses_split_knobs_the_kernels_reject(monkeypatch):
+    """A split-K knob outside what the in-kernel finalisation takes (PG_SPLIT_DOWN=16 at batch 16 once made
+    pg_gemm_fused(F32_FIN) fail at launch) is refused when the engine is built, before any launch."""
+    from pghip import configs, engine, weights
+    cfg = configs.TINY
+    W = synth.generate_state_dict(cfg)
+    P = weights.PackedWeights(cfg, lambda k: torch.from_numpy(W[k]), device="cpu")
+    engine.PaliGemmaEngine(cfg, P, device="cpu")
+    monkeypatch.setenv("PG_SPLIT_DOWN", "16")
+    with pytest.raises(ValueError, match="split-K 16"):
+        engine.PaliGemmaEngine(cfg, P, device="cpu")

@@ -15,16 +15,17 @@ def close(a, b, tol=2e-5):
     assert err < tol, f"scaled max error {err:.3e} >= {tol:.1e}"
 
 
-def _tiny_oracle(recompute=True):
-    cfg = configs.TINY
+def _tiny_oracle(recompute=True, name="tiny"):
+    cfg = configs.CONFIGS[name]
     return O.PaliGemmaOracle(cfg, synth.generate_state_dict(cfg), recompute_vision=recompute)
 
 
-@pytest.mark.parametrize("B", [1, 2])
-def test_tiny_prefill_matches_reference(golden, B):
-    g = golden("tiny")
+@pytest.mark.parametrize("name,B", [("tiny", 1), ("tiny", 2), ("tiny8", 1), ("tiny8", 8)])
+def test_tiny_prefill_matches_reference(golden, name, B):
+    """tiny (4 q heads) and tiny8 (8 q heads, the tensor-parallel toy: B = 8 is one image per rank at TP=8)."""
+    g = golden(name)
     p = f"b{B}_"
-    orc = _tiny_oracle()
+    orc = _tiny_oracle(name=name)
     feats = orc.image_features(g[p + "pixel_values"])
     v = O.siglip_vision_model(orc.W, orc.vcfg, g[p + "pixel_values"])
     close(v, g[p + "vision_out"])
@@ -39,9 +40,10 @@ def test_tiny_prefill_matches_reference(golden, B):
     close(kv.v_cache[-1], g[p + "v_cache0"])
 
 
-def test_tiny_greedy_loop_matches_reference(golden):
-    g = golden("tiny")
-    orc = _tiny_oracle()
+@pytest.mark.parametrize("name", ["tiny", "tiny8"])
+def test_tiny_greedy_loop_matches_reference(golden, name):
+    g = golden(name)
+    orc = _tiny_oracle(name=name)
     ids, logits = O.generate(orc, g["b1_input_ids"], g["b1_pixel_values"], np.ones_like(g["b1_input_ids"]),
                              max_tokens=len(g["greedy_ids"]), record_logits=True)
     assert ids == g["greedy_ids"].tolist()

@@ -1,5 +1,5 @@
-"""Tensor-parallel engine on the HIP device: two ranks share one MI355X over the gloo transport
-(RCCL refuses two ranks on one GPU; the 8-GPU RCCL run is the driver's scaling bench).  Checks the
+"""Tensor-parallel engine on the HIP device: 2, 4 or 8 ranks share one MI355X over the gloo transport or the xGMI
+exchange (RCCL refuses two ranks on one GPU; the 8-GPU RCCL run is the driver's scaling bench).  Checks the
 sharded kernels, the partial-sum all-reduces and the vocabulary-parallel greedy / top-p paths
 against the reference's golden vectors and the single-rank engine.  Tolerance as
 tests/test_engine_gpu.py (scaled max error < 3e-2 vs the fp32 reference); TP vs single-rank
@@ -52,20 +52,72 @@ def test_xgmi_allreduce_ranks_on_one_device(tmp_path, world):
     assert len({o["digest"] for o in res}) == 1
 
 
-@pytest.mark.parametrize("comm", ["gloo", "xgmi"])
-def test_tp2_engine_on_one_device(tmp_path, comm):
+# (config, ranks, transport, prefill chunk rows, fp8): TP 2 on tiny (4 q heads); TP 4 / 8 on tiny8 (8 q heads: one per
+# rank at TP 8, the split of BASELINE configs[4]); chunk rows 8 make every prefill o_proj / down_proj run as row chunks
+# whose all-reduces are issued asynchronously (xGMI side stream / async gloo) while the next chunk's GEMM runs.
+TP_CASES = [("tiny", 2, "gloo", None, False), ("tiny", 2, "xgmi", None, False),
+            ("tiny8", 4, "xgmi", 8, False), ("tiny8", 8, "xgmi", None, False), ("tiny8", 8, "gloo", 8, False),
+            ("tiny8", 8, "xgmi", 8, True)]
+
+
+@pytest.mark.parametrize("cfg,world,comm,chunk,fp8", TP_CASES, ids=lambda v: str(v))
+def test_tp_engine_on_one_device(tmp_path, cfg, world, comm, chunk, fp8):
+    """The tensor-parallel engine with `world` ranks sharing the device, against the reference's goldens (prefill
+    logits of every golden batch: B = 8 at TP 8 runs the SigLIP tower data-parallel, one image per rank; the 12
+    greedy ids of the reference's own loop) and the single-rank engine (prefill, 19 teacher-forced decode steps,
+    top-p draws with the same uniforms).  fp8: every linear of more than 16 rows on the fp8 MFMA, TP and single rank
+    each within the fp8 bound of the fp32 references (they quantise different weight slices), plus a 24-row
+    teacher-forced decode (the fp8 decode path) against the oracle."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
-    res = _launch("tp_worker.py", tmp_path, TP_COMM=comm)
+    env = dict(TP_COMM=comm, TP_CFG=cfg)
+    if chunk:
+        env["TP_CHUNK"] = str(chunk)
+    if fp8:
+        env["TP_FP8"] = "1"
+    res = _launch("tp_worker.py", tmp_path, nproc=world, **env)
+    tol = 0.12 if fp8 else 3e-2                  # vs the fp32 reference (tests/test_engine_gpu.py)
     for o in res:
         assert o["xgmi_err"] == 0, o
         assert o["graph"] == (comm == "xgmi"), o
-        assert o["prefill_err_b1"] < 3e-2 and o["prefill_err_b2"] < 3e-2, o
-        assert o["greedy"] == o["greedy_ref"], o
-        assert o["decode_slice_err"] < 5e-3, o
-        assert o["decode_argmax_agree"], o
-        assert o["sampled_tp"] == o["sampled_solo"], o
-    assert res[0]["greedy"] == res[1]["greedy"] and res[0]["sampled_tp"] == res[1]["sampled_tp"]
+        assert o["world"] == world and (chunk is None or o["chunk_rows"] == chunk), o
+        pre = [k for k in o if k.startswith("prefill_err_b")]
+        assert pre and all(o[k] < tol for k in pre), o
+        assert all(o[k] < (tol if fp8 else 1e-2) for k in o if k.startswith("prefill_err_vs_solo")), o
+        if cfg == "tiny8" and world == 8:
+            assert 8 in o["vision_dp"], o             # one image per rank through the data-parallel SigLIP
+        if fp8:
+            assert o["decode_slice_err"] < tol, o
+            assert o["fp8_decode24_err"] < tol, o
+        else:
+            assert o["greedy"] == o["greedy_ref"], o
+            assert o["decode_slice_err"] < 5e-3, o
+            assert o["decode_argmax_agree"], o
+            assert o["sampled_tp"] == o["sampled_solo"], o
+    assert all(o["greedy"] == res[0]["greedy"] and o["sampled_tp"] == res[0]["sampled_tp"] for o in res)
+
+
+@pytest.mark.slow
+def test_tp8_pt896_fp8_batch8(tmp_path):
+    """BASELINE configs[4]'s model and split: PaliGemma-3B-pt-896 with fp8 Gemma linears at TP=8 (one q head, 2048
+    intermediate columns and 32,152 vocabulary rows per rank; modeling_gemma.py:205-218, 255-259, 356, 523), eight
+    ranks on one device, batch 8 (one image per rank through the data-parallel SigLIP).  Prefill (32,832 rows, the
+    all-reduces in 4096-row chunks) and 3 teacher-forced decode steps: row 0 against the reference's pt-896 request
+    (the fp8 bound of tests/test_large_gpu.py, 30% of the top-64 scale), every row against the single-rank fp8 engine
+    (the two quantise different weight slices: the same 30% bound, the same top-1 wherever the single-rank margin
+    exceeds 5% of the scale)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896")
+    for o in res:
+        assert o["xgmi_err"] == 0 and o["vision_dp"], o
+        assert o["ref_top64_err"] < 0.30, o
+        for t, (got, want, m, e) in enumerate(zip(o["ref_top1"], o["ref_ids"], o["ref_margin"], o["ref_top64_abs"])):
+            if m > 2 * e:                          # as test_large_gpu._check_step
+                assert got == want, (t, o)
+    r0 = res[0]
+    assert r0["solo_ref_top64_err"] < 0.30 and r0["vs_solo_err"] < 0.30 and r0["vs_solo_top1_agree"], r0
+    assert all(o["ref_top1"] == r0["ref_top1"] for o in res)
 
 
 @pytest.mark.slow

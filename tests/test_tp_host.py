@@ -1,4 +1,4 @@
-"""Tensor-parallel sharding on the CPU (gloo, world size 2 and 4): the per-rank weight slices
+"""Tensor-parallel sharding on the CPU (gloo, world size 2, 4 and 8): the per-rank weight slices
 PackedWeights(tp_rank, tp_world) produces, run through the oracle's own layer functions and summed
 with a torch.distributed SUM all-reduce — exactly the data flow of the HIP engine under TP — must
 reproduce the unsharded oracle layer (modeling_gemma.py:264-358 attention, :210-218 MLP, :530-534
@@ -43,7 +43,7 @@ def _unpack_layer(P, i):
 
 
 def _worker(rank, world, port, cfg_name):
-    from pghip.weights import PackedWeights
+    from pghip.weights import PackedWeights, frag_unpack
     dist.init_process_group("gloo", rank=rank, world_size=world, init_method=f"tcp://127.0.0.1:{port}")
     try:
         cfg = ocfg.CONFIGS[cfg_name]
@@ -66,36 +66,64 @@ def _worker(rank, world, port, cfg_name):
             dist.all_reduce(t)
             full = O.gemma_attention(W, lp + "self_attn.", tc, i, x, pos, mask, None)
             np.testing.assert_allclose(t.numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
-            part = O.gemma_mlp(Wl, lp + "mlp.", x)
+            # the MLP's row-parallel partial sum, all-reduced in row chunks issued asynchronously before any is
+            # waited on (engine._row_parallel at T >= 2 * AR_CHUNK_ROWS): the same sums as one all-reduce
+            part = O.gemma_mlp(Wl, lp + "mlp.", x).reshape(B * L, H)
             t = torch.from_numpy(np.ascontiguousarray(part))
-            dist.all_reduce(t)
-            full = O.gemma_mlp(W, lp + "mlp.", x)
+            bounds = [B * L * c // 3 for c in range(4)]
+            works = [dist.all_reduce(t[r0:r1], async_op=True) for r0, r1 in zip(bounds[:-1], bounds[1:])]
+            for wk in works:
+                wk.wait()
+            full = O.gemma_mlp(W, lp + "mlp.", x).reshape(B * L, H)
             np.testing.assert_allclose(t.numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
-        # vocabulary-parallel lm_head: each rank fills its slot of a zeroed buffer, SUM all-reduce gathers
+        # vocabulary-parallel lm_head (engine.lm_head): every rank's slice [rows][vocab_local_pad], all-gathered in
+        # rank order, the padding dropped, slices concatenated
         xr = x.reshape(-1, H)
-        g = torch.zeros(xr.shape[0], world, P.vocab_local_pad)
-        from pghip.weights import frag_unpack
+        rows = xr.shape[0]
         lm_w = frag_unpack(P.lm_w) if P.frag else P.lm_w
-        g[:, rank] = torch.from_numpy(xr) @ lm_w.float().T + P.lm_bias
-        dist.all_reduce(g)
+        loc = (torch.from_numpy(xr) @ lm_w.float().T + P.lm_bias).contiguous()
+        g = torch.empty(world, rows, P.vocab_local_pad)
+        dist.all_gather_into_tensor(g.view(-1), loc.view(-1))
+        got = g[:, :, :P.vocab_local].permute(1, 0, 2).reshape(rows, -1)
         full = xr @ W["language_model.model.embed_tokens.weight"].T + W["language_model.lm_head.bias"]
-        np.testing.assert_allclose(g[:, :, :P.vocab_local].reshape(xr.shape[0], -1).numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
-        # greedy merge of per-rank (max, first index) pairs == global argmax (lowest index on ties)
-        loc = g[:, rank, :P.vocab_local]
-        pairs = torch.zeros(world, xr.shape[0], 2)
+        np.testing.assert_allclose(got.numpy(), full, rtol=0, atol=2e-5 * np.abs(full).max())
+        # greedy (engine.decode_step, pg_argmax_pairs + pg_argmax_merge): each rank's (max, first global index)
+        # pair per row, all-gathered [W][rows][2]; the merge keeps the largest value, the lowest index on ties.
+        # Ties across ranks are forced on row 0 (the same value planted in every rank's slice) -> rank 0's index.
+        loc = loc[:, :P.vocab_local].clone()
+        loc[0, 5] = 1e4
         mx, ix = loc.max(-1)
-        pairs[rank, :, 0], pairs[rank, :, 1] = mx, (ix + P.vocab_offset).float()
-        dist.all_reduce(pairs)
+        mine = torch.stack([mx, (ix + P.vocab_offset).float()], -1).contiguous()
+        pairs = torch.empty(world, rows, 2)
+        dist.all_gather_into_tensor(pairs.view(-1), mine.view(-1))
         best = pairs[:, :, 0].argmax(0)                                   # first rank holding the max
-        merged = pairs[best, torch.arange(xr.shape[0]), 1].long()
-        assert merged.tolist() == full.argmax(-1).tolist()
+        merged = pairs[best, torch.arange(rows), 1].long()
+        ref = full.copy()
+        for r in range(world):
+            ref[0, r * P.vocab_local + 5] = 1e4
+        assert merged.tolist() == ref.argmax(-1).tolist()
+        assert merged[0].item() == 5
+        # data-parallel SigLIP (engine.vision with B >= W, B % W == 0): rank r encodes images [r*B/W, (r+1)*B/W)
+        # and the projected features are all-gathered in rank order = image order
+        vcfg = cfg["vision_config"]
+        n_img = (vcfg["image_size"] // vcfg["patch_size"]) ** 2
+        Bi = world
+        px = rng.standard_normal((Bi, 3, vcfg["image_size"], vcfg["image_size"])).astype(np.float32)
+        Bl = Bi // world
+        mine = O.multi_modal_projector(W, O.siglip_vision_model(W, vcfg, px[rank * Bl:(rank + 1) * Bl]))
+        feats = torch.empty(Bi * n_img * mine.shape[-1])
+        dist.all_gather_into_tensor(feats, torch.from_numpy(np.ascontiguousarray(mine)).view(-1))
+        full = O.multi_modal_projector(W, O.siglip_vision_model(W, vcfg, px))
+        np.testing.assert_allclose(feats.view(full.shape).numpy(), full, rtol=0, atol=1e-5 * np.abs(full).max())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_tp_sharding_matches_unsharded_oracle(world):
-    mp.spawn(_worker, args=(world, _free_port(), "tiny"), nprocs=world, join=True)
+@pytest.mark.parametrize("cfg_name,world", [("tiny", 2), ("tiny", 4), ("tiny8", 2), ("tiny8", 4), ("tiny8", 8)])
+def test_tp_sharding_matches_unsharded_oracle(cfg_name, world):
+    """world 8 on tiny8 = one q head, 80 intermediate columns and 38 vocabulary rows per rank: the TP=8 split of
+    BASELINE configs[4] (modeling_gemma.py:205-218 MLP, :255-259 q/k/v/o, :484/:523 lm_head)."""
+    mp.spawn(_worker, args=(world, _free_port(), cfg_name), nprocs=world, join=True)
 
 
 def test_tp_rejects_bad_split():

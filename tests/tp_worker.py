@@ -1,8 +1,10 @@
-"""Rank body of tests/test_tp_gpu.py (launched by torch.distributed.run, 2 ranks on one HIP device,
-gloo transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden
-vectors and the single-rank engine.  TP_CFG=tiny (default) uses the tiny fixtures; TP_CFG=pt-224 runs the full-size
-PaliGemma-3B-224 (BASELINE configs[3]'s mix-224 architecture) against tests/golden/pt224.npz.  Writes one JSON
-verdict per rank to $TP_OUT/rank<r>.json."""
+"""Rank body of tests/test_tp_gpu.py (launched by torch.distributed.run, 2 / 4 / 8 ranks on one HIP device, gloo
+transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden vectors
+and the single-rank engine.  TP_CFG=tiny (default) / tiny8 use the tiny fixtures (tiny8: the 8-head toy for TP up to
+8); TP_CFG=pt-224 runs the full-size PaliGemma-3B-224 (BASELINE configs[3]'s mix-224 architecture) against
+tests/golden/pt224wc.npz; TP_CFG=pt-896 runs BASELINE configs[4]'s model (pt-896, fp8 Gemma linears) at batch 8
+against the single-rank engine and tests/golden/pt896.npz.  Writes one JSON verdict per rank to
+$TP_OUT/rank<r>.json."""
 import json
 import os
 import sys
@@ -50,34 +52,59 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
+    name = os.environ.get("TP_CFG", "tiny")
+    if name == "pt-896":
+        return full_size_896(rank, world)
+    if name not in ("tiny", "tiny8"):
+        return full_size(rank, world, name)
+    return tiny(rank, world, name)
+
+
+def tiny(rank, world, name):
+    """TP_CFG=tiny (4 q heads: TP 2 / 4) or tiny8 (8 q heads, hidden 1024: TP 2 / 4 / 8; at TP=8 every rank holds one
+    q head, 80 intermediate columns and 38 vocabulary rows, as configs[4]'s split of the real model).  TP_CHUNK=n
+    cuts every prefill row-parallel linear into row chunks from 2n rows on (engine._row_parallel: chunk c's all-reduce
+    issued asynchronously -- on the xGMI side stream or as an async gloo op -- while chunk c+1's GEMM runs).
+    TP_FP8=1 packs fp8 Gemma linears (every linear of more than 16 rows runs on the block-scaled fp8 MFMA) and adds a
+    24-row teacher-forced decode (fp8 decode path) against the oracle."""
     from pghip import configs, engine, synthetic, weights
     from pghip.tp import TPComm, XgmiComm
-    if os.environ.get("TP_CFG", "tiny") != "tiny":
-        return full_size(rank, world, os.environ["TP_CFG"])
-    cfg = configs.TINY
+    from oracle import configs as ocfg, synth
+    from oracle import paligemma_oracle as O
+    cfg = configs.CONFIGS[name]
+    fp8 = os.environ.get("TP_FP8") == "1"
     sd = synthetic.SyntheticStateDict(cfg)
     comm = XgmiComm(cap=1 << 20) if os.environ.get("TP_COMM") == "xgmi" else TPComm()
-    tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world),
-                                comm=comm)
-    solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__))
-    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "tiny.npz")))
-    out = {"rank": rank, "world": world, "comm": type(comm).__name__, "graph": comm.capturable}
-    for B in (1, 2):
+    tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world,
+                                                           fp8=fp8), comm=comm)
+    if os.environ.get("TP_CHUNK"):
+        tp.AR_CHUNK_ROWS = int(os.environ["TP_CHUNK"])
+    solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=fp8))
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz")))
+    out = {"rank": rank, "world": world, "comm": type(comm).__name__, "graph": comm.capturable, "cfg": name,
+           "fp8": fp8, "chunk_rows": tp.AR_CHUNK_ROWS, "vision_dp": []}
+    for B in sorted(int(k[1:-len("_logits")]) for k in g if k.startswith("b") and k.endswith("_logits")):
         p = f"b{B}_"
         ids = torch.from_numpy(g[p + "input_ids"]).cuda()
         px = torch.from_numpy(g[p + "pixel_values"]).cuda()
         Bv, L = ids.shape
-        cache = tp.new_cache(Bv, L + 8)
-        resid = torch.empty(Bv * L, tp.w.hidden, device="cuda")
-        tp.embed_merge(ids, tp.vision(px), resid)
-        pos = torch.arange(1, L + 1, dtype=torch.int32).repeat(Bv, 1)
-        logits, _ = tp.gemma_prefill(resid, pos, cache, Bv, L)
-        out[f"prefill_err_b{B}"] = err(logits.cpu().numpy(), g[p + "logits"].reshape(Bv * L, -1))
+        lg = []
+        for e in (tp, solo):
+            cache = e.new_cache(Bv, L + 8)
+            resid = torch.empty(Bv * L, e.w.hidden, device="cuda")
+            e.embed_merge(ids, e.vision(px), resid)
+            pos = torch.arange(1, L + 1, dtype=torch.int32).repeat(Bv, 1)
+            lg.append(e.gemma_prefill(resid, pos, cache, Bv, L)[0].clone())
+        out[f"prefill_err_b{B}"] = err(lg[0].cpu().numpy(), g[p + "logits"].reshape(Bv * L, -1))
+        out[f"prefill_err_vs_solo_b{B}"] = err(lg[0].cpu().numpy(), lg[1].cpu().numpy())
+        if Bv >= world and Bv % world == 0:
+            out["vision_dp"].append(B)
     ids = torch.from_numpy(g["b1_input_ids"]).cuda()
     px = torch.from_numpy(g["b1_pixel_values"]).cuda()
     am = torch.ones_like(ids)
     out["greedy"] = tp.generate(ids, px, am, len(g["greedy_ids"]))[0].tolist()
     out["greedy_ref"] = g["greedy_ids"].tolist()
+    out["greedy_solo"] = solo.generate(ids, px, am, len(g["greedy_ids"]))[0].tolist()
     # long teacher-forced decode: TP logits (gathered full vocabulary) vs the single-rank engine
     steps = 20
     caches, nxts, feats = [], [], []
@@ -86,8 +113,9 @@ def main():
         caches.append(c), nxts.append(n), feats.append(f)
     st = [e.decode_state(1, c, n, steps) for e, c, n in zip((tp, solo), caches, nxts)]
     worst, agree = 0.0, True
+    V = tp.w.vocab
     for t in range(steps - 1):
-        tok = 7 + 13 * t
+        tok = (7 + 13 * t) % V
         lgs = []
         for e, s, c, f in zip((tp, solo), st, caches, feats):
             s["ids"].fill_(tok)
@@ -105,6 +133,35 @@ def main():
                                     stop_token=None)[0].tolist()
     out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
                                         stop_token=None)[0].tolist()
+    if fp8:
+        # 24 rows (> 16: the fp8 decode path) of 24 different images, teacher-forced 3 steps, against the fp32 oracle
+        # (TP and single rank quantise different weight slices, so each is held to the fp8 bound on its own)
+        ocfg_ = ocfg.CONFIGS[name]
+        orc = O.PaliGemmaOracle(ocfg_, synth.generate_state_dict(ocfg_), recompute_vision=False)
+        Bd, size = 24, ocfg_["vision_config"]["image_size"]
+        rng = np.random.default_rng(11)
+        pxb = rng.standard_normal((Bd, 3, size, size)).astype(np.float32)
+        ids_b = np.repeat(g["b1_input_ids"], Bd, 0)
+        amb = np.ones_like(ids_b)
+        c, f, lg0, n = tp.prefill_request(torch.from_numpy(ids_b).cuda(), torch.from_numpy(pxb).cuda(),
+                                          torch.from_numpy(amb).cuda(), 4)
+        s_ = tp.decode_state(Bd, c, n, 4)
+        samp = dict(do_sample=True, temperature=0.8, top_p=0.9, uniforms=torch.full((5, Bd), 0.5, device="cuda"))
+        kvs = [O.KVCache() for _ in range(Bd)]
+        ref = [orc.forward(ids_b[b:b + 1], pxb[b:b + 1], amb[b:b + 1], kvs[b], logits_rows=slice(-1, None))
+               ["logits"][0, -1] for b in range(Bd)]
+        fe = [err(lg0[b].cpu().numpy(), ref[b]) for b in range(Bd)]
+        for t in range(3):
+            tok = [5 + (7 * b + 11 * t) % 250 for b in range(Bd)]         # ordinary text ids (no image / pad id)
+            s_["ids"].copy_(torch.tensor(tok, device="cuda"))
+            s_["step"].zero_()
+            lgd = tp.decode_step(s_, c, f, samp).clone().cpu().numpy()
+            L1 = ids_b.shape[1] + t + 1
+            for b in range(Bd):
+                r = orc.forward(np.array([[tok[b]]]), pxb[b:b + 1], np.ones((1, L1), np.int64), kvs[b],
+                                logits_rows=slice(-1, None))["logits"][0, -1]
+                fe.append(err(lgd[b], r))
+        out["fp8_decode24_err"] = max(fe)
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
     if isinstance(comm, XgmiComm):
@@ -189,6 +246,82 @@ def full_size(rank, world, name):
         comm.close()
     with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def full_size_896(rank, world):
+    """BASELINE configs[4]'s model at TP = world: PaliGemma-3B-pt-896 (4096 image tokens), fp8 e4m3 Gemma linears,
+    batch 8 = one image per rank at TP=8 through the data-parallel SigLIP tower (its projected features all-gathered
+    in image order).  Row 0 is the reference's pt-896 request (tests/golden/pt896.npz), rows 1-7 other images.  The
+    32,832-row prefill cuts every o_proj / down_proj into 4096-row chunks whose all-reduces overlap the next chunk's
+    GEMM (engine._row_parallel; 33.5 MB chunks exceed the xGMI exchange here, so they travel over the process group),
+    then 3 teacher-forced decode steps (the reference's greedy ids; decode all-reduces over the xGMI exchange, graph
+    capturable).  Rank 0 then runs the same requests on the single-rank fp8 engine."""
+    from PIL import Image
+    from pghip import configs, engine, synthetic, weights
+    from pghip.tp import TPComm, XgmiComm
+    from processing_paligemma import process_images
+    cfg = configs.PT_896
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "pt896.npz")))
+    sd = synthetic.SyntheticStateDict(cfg)
+    comm = XgmiComm(cap=1 << 20) if os.environ.get("TP_COMM") == "xgmi" else TPComm()
+    tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world,
+                                                           fp8=True), comm=comm)
+    B = 8
+    seeds = [int(g["seeds"][0])] + [2001 + b for b in range(1, B)]
+    pv = []
+    for sd_ in seeds:
+        img = np.random.default_rng(sd_).integers(0, 256, (1, 896, 896, 3), dtype=np.uint8)
+        pv.append(np.stack(process_images([Image.fromarray(img[0])], 896, 1 / 255.0, Image.Resampling.BICUBIC)))
+    pv = np.concatenate(pv).astype(np.float32)
+    assert np.array_equal(pv[0].reshape(-1)[::9973], g["i0_pixel_sample"])
+    ids = torch.from_numpy(np.concatenate([g["i0_input_ids"]] * B)).cuda()
+    px = torch.from_numpy(pv).cuda()
+    ref_ids = g["i0_greedy_ids"].tolist()
+    steps = len(ref_ids)
+
+    def run(e):
+        cache, feats, logits, nxt = e.prefill_request(ids, px, torch.ones_like(ids), steps + 2)
+        st = e.decode_state(B, cache, nxt, steps + 2)
+        samp = dict(do_sample=True, temperature=0.8, top_p=0.9, uniforms=torch.full((steps + 3, B), 0.5, device="cuda"))
+        out = [logits.float().cpu().numpy()]
+        for t in range(1, steps):
+            st["ids"].fill_(ref_ids[t - 1])
+            st["step"].zero_()
+            out.append(e.decode_step(st, cache, feats, samp).float().cpu().numpy())
+        torch.cuda.synchronize()
+        return np.stack(out)                                        # [steps][B][V]
+    lg_tp = run(tp)
+    res = {"rank": rank, "world": world, "comm": type(comm).__name__, "chunks": tp.AR_CHUNK_ROWS,
+           "vision_dp": B >= world and B % world == 0}
+    torch.cuda.synchronize()
+    res["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+
+    def top64(lg, t, scaled=True):
+        top_ids, top_v = g["i0_step_top_ids"][t], g["i0_step_top_values"][t]
+        return float(np.abs(lg[top_ids] - top_v).max() / (np.abs(top_v).max() if scaled else 1.0))
+    res["ref_top64_err"] = max(top64(lg_tp[t, 0], t) for t in range(steps))
+    res["ref_top64_abs"] = [top64(lg_tp[t, 0], t, False) for t in range(steps)]
+    res["ref_top1"] = [int(lg_tp[t, 0].argmax()) for t in range(steps)]
+    res["ref_ids"] = ref_ids
+    res["ref_margin"] = [float(m) for m in g["i0_margin"]]
+    if rank == 0:
+        del tp
+        torch.cuda.empty_cache()
+        solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=True))
+        lg_solo = run(solo)
+        res["solo_ref_top64_err"] = max(top64(lg_solo[t, 0], t) for t in range(steps))
+        res["vs_solo_err"] = max(err(lg_tp[t], lg_solo[t]) for t in range(steps))
+        res["vs_solo_top1_agree"] = all(
+            int(lg_tp[t, b].argmax()) == int(lg_solo[t, b].argmax()) or
+            np.sort(lg_solo[t, b])[-1] - np.sort(lg_solo[t, b])[-2] < 0.05 * np.abs(lg_solo[t, b]).max()
+            for t in range(steps) for b in range(B))
+        del solo
+    if isinstance(comm, XgmiComm):
+        comm.close()
+    with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
     dist.barrier()
     dist.destroy_process_group()
 
