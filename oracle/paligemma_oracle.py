@@ -47,6 +47,37 @@ class bf16_operands:
         _BF16_OPERANDS = self._old
 
 
+# fp8-operand emulation (test aid, BASELINE configs[4]): when on, the Gemma decoder linears (q/k/v/o, gate/up/down;
+# not the lm_head, which the HIP path keeps bf16) multiply e4m3 operands -- activation rows and weight output rows
+# each scaled by max|row| / 448 (weights.quant_rows_fp8 / pg_quant_fp8's rule) -- whenever a call has more than
+# `min_rows` rows (the HIP path runs fp8 for linears of more than 16 rows: prefill, and decode at batch > 16).
+# The fp8 path's intrinsic sensitivity on a model then bounds the HIP fp8 path's distance to the fp32 reference.
+_FP8_MIN_ROWS = None
+
+
+class fp8_operands:
+    def __init__(self, min_rows: int = 16):
+        self.min_rows = min_rows
+
+    def __enter__(self):
+        global _FP8_MIN_ROWS
+        self._old, _FP8_MIN_ROWS = _FP8_MIN_ROWS, self.min_rows
+
+    def __exit__(self, *a):
+        global _FP8_MIN_ROWS
+        _FP8_MIN_ROWS = self._old
+
+
+def q8_rows(x: np.ndarray) -> np.ndarray:
+    """Per-row e4m3 round trip: x ~= e4m3(x / s) * s, s = max|row| / 448 (1 for a zero row)."""
+    import torch
+    x2 = np.ascontiguousarray(x, dtype=F32).reshape(-1, x.shape[-1])
+    amax = np.abs(x2).max(axis=1, keepdims=True)
+    s = np.where(amax > 0, amax / F32(448.0), F32(1.0)).astype(F32)
+    q = torch.from_numpy(np.clip(x2 / s, -448.0, 448.0)).to(torch.float8_e4m3fn).float().numpy()
+    return (q * s).reshape(x.shape).astype(F32)
+
+
 def q16(x: np.ndarray) -> np.ndarray:
     if not _BF16_OPERANDS:
         return x
@@ -80,9 +111,12 @@ def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float) -> np.nd
     return (y * w + b).astype(F32)
 
 
-def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None) -> np.ndarray:
-    """nn.Linear: x @ w.T + b."""
-    y = q16(x) @ w.T
+def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: bool = False) -> np.ndarray:
+    """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation.)"""
+    if gemma and _FP8_MIN_ROWS is not None and x.size // x.shape[-1] > _FP8_MIN_ROWS:
+        y = q8_rows(x) @ q8_rows(w).T
+    else:
+        y = q16(x) @ w.T
     if b is not None:
         y = y + b
     return y.astype(F32, copy=False)
@@ -217,9 +251,9 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     B, L, _ = x.shape
     nh, nkv = tcfg["num_attention_heads"], tcfg["num_key_value_heads"]
     hd = tcfg.get("head_dim", 256)
-    k = linear(x, W[lp + "k_proj.weight"])                              # :274
-    v = linear(x, W[lp + "v_proj.weight"])                              # :276
-    q = linear(x, W[lp + "q_proj.weight"])                              # :278
+    k = linear(x, W[lp + "k_proj.weight"], gemma=True)                              # :274
+    v = linear(x, W[lp + "v_proj.weight"], gemma=True)                              # :276
+    q = linear(x, W[lp + "q_proj.weight"], gemma=True)                              # :278
     k = q16(k).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)             # :285-287
     v = q16(v).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)
     q = q16(q).reshape(B, L, nh, hd).transpose(0, 2, 1, 3)
@@ -240,14 +274,14 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     if o.shape != (B, nh, L, hd):                                       # :341-345
         raise ValueError("Size Mismatch")
     o = o.transpose(0, 2, 1, 3).reshape(B, L, -1)                       # :354-355
-    return linear(o, W[lp + "o_proj.weight"])                           # :356
+    return linear(o, W[lp + "o_proj.weight"], gemma=True)                           # :356
 
 
 def gemma_mlp(W: dict, lp: str, x: np.ndarray) -> np.ndarray:
     """GemmaMLP.forward (modeling_gemma.py:210-218)."""
-    y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"]))
-    u = linear(x, W[lp + "up_proj.weight"])
-    return linear(y * u, W[lp + "down_proj.weight"])
+    y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"], gemma=True))
+    u = linear(x, W[lp + "up_proj.weight"], gemma=True)
+    return linear(y * u, W[lp + "down_proj.weight"], gemma=True)
 
 
 def gemma_model(W: dict, tcfg: dict, input_embeds: np.ndarray, position_ids, mask, kv_cache,

@@ -195,19 +195,22 @@ class PaliGemmaEngine:
 
     # ------------------------------------------------------------------ vision tower
     def vision(self, pixel_values: torch.Tensor, want_hidden: bool = False, taps: Optional[list] = None,
-               _local: bool = False):
+               _split_batch: Optional[int] = None):
         """SiglipVisionModel.forward + projector (modeling_siglip.py:312-334, modeling_paligemma.py:60-65).
         Returns image features fp32 [B*N][P] (projector output, unscaled) and optionally the
-        post-LN vision output fp32 [B*N][hv]."""
+        post-LN vision output fp32 [B*N][hv].  _split_batch (the data-parallel call of a rank's slice): choose the
+        split-K and attention key splits as for a batch of that many images, so that each image's features are
+        bit-identical to the single-rank run over the whole batch."""
         w = self.w
         px = pixel_values.to(device=self.device, dtype=torch.float32).contiguous()
         B = px.shape[0]
-        if (not _local and self.tp > 1 and self.VISION_DP and B >= self.tp and B % self.tp == 0 and not want_hidden
-                and taps is None and w.proj_w is not None):
+        if (_split_batch is None and self.tp > 1 and self.VISION_DP and B >= self.tp and B % self.tp == 0
+                and not want_hidden and taps is None and w.proj_w is not None):
             # data-parallel over the images (output-invariant, SURVEY.md §8(e)): this rank encodes its B/W images,
-            # then the projected features [B*N][P] are all-gathered in rank order = image order
+            # then the projected features [B*N][P] are all-gathered in rank order = image order.  The rank-local
+            # call takes the whole batch's split choices, so the features equal the replicated run's bit for bit
             Bl = B // self.tp
-            mine = self.vision(px[self.comm.rank * Bl:(self.comm.rank + 1) * Bl], _local=True)
+            mine = self.vision(px[self.comm.rank * Bl:(self.comm.rank + 1) * Bl], _split_batch=B)
             feats = torch.empty(B * w.n_img, w.proj_dim, dtype=torch.float32, device=self.device)
             self.comm.all_gather(feats, mine)
             return feats
@@ -224,22 +227,23 @@ class PaliGemmaEngine:
         vt = self._buf("v_vt", (hv, M + 32), torch.bfloat16)            # rows padded: attention reads 32-key blocks
         attn = self._buf("v_attn", (M, hv), torch.bfloat16)
         h = self._buf("v_h", (M, w.v_inter), torch.bfloat16)
-        s_o = ops.gemm_ksplit(M, hv, hv)
-        s_2 = ops.gemm_ksplit(M, hv, w.v_inter)
-        ks_v = self._key_split_args("v", B, N, N, nh, nh, hd)
+        Bs = _split_batch or B                                            # the batch the splits are chosen for
+        s_o = ops.gemm_ksplit(Bs * N, hv, hv)
+        s_2 = ops.gemm_ksplit(Bs * N, hv, w.v_inter)
+        ks_v = self._key_split_args("v", Bs, N, N, nh, nh, hd)
         part = self._buf("v_part", (max(s_o, s_2), M, hv), torch.float32)
         ns = 0
         for L in w.vl:
             ops.norm_residual(resid, L["ln1_w"], b=L["ln1_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
                               nsplit=ns, out=xn)
             ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M + 32,
-                     aux_n=2 * hv)
+                     aux_n=2 * hv, split_m=Bs * N)
             ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
                           B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5), **ks_v)
             self._gemm_cols(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
             ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
                               nsplit=s_o, out=xn)
-            self._gemm_cols(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"])
+            self._gemm_cols(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"], split_m=Bs * N)
             self._gemm_cols(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
             ns = s_2
             if taps is not None:                                          # debug: residual after the layer
@@ -403,15 +407,18 @@ class PaliGemmaEngine:
             return ops.gemm_fused(x, W, out, fa, epi=epi | flag, M=M)
         return ops.gemm(x, W, out, epi=epi | flag, ksplit=ksplit)
 
-    def _gemm_cols(self, A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int, bias=None, ksplit: int = 1):
+    def _gemm_cols(self, A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int, bias=None, ksplit: int = 1,
+                   split_m: Optional[int] = None):
         """ops.gemm; or, when the last 256-column tile is ragged and dropping it saves a round of CUs, the whole
         256-column tiles and the remaining columns as two GEMMs into the same output (column views: same ldc
         and slab stride).  SigLIP o / fc1 / fc2 at pt-448 x16: 320 -> 256, 1088 -> 1024, 640 -> 512 tiles."""
         Nh = self._col_head(A.shape[0], W.shape[0], ksplit) if self.COL_BLOCKS else 0
         if not Nh:
-            return ops.gemm(A, W, out, epi=epi, bias=bias, ksplit=ksplit)
-        ops.gemm(A, W[:Nh], out[..., :Nh], epi=epi, bias=None if bias is None else bias[:Nh], ksplit=ksplit)
-        return ops.gemm(A, W[Nh:], out[..., Nh:], epi=epi, bias=None if bias is None else bias[Nh:], ksplit=ksplit)
+            return ops.gemm(A, W, out, epi=epi, bias=bias, ksplit=ksplit, split_m=split_m)
+        ops.gemm(A, W[:Nh], out[..., :Nh], epi=epi, bias=None if bias is None else bias[:Nh], ksplit=ksplit,
+                 split_m=split_m)
+        return ops.gemm(A, W[Nh:], out[..., Nh:], epi=epi, bias=None if bias is None else bias[Nh:], ksplit=ksplit,
+                        split_m=split_m)
 
     @staticmethod
     def _col_head(M: int, N: int, ksplit: int, cus: int = ops.CUS) -> int:

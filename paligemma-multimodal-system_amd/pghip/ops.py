@@ -45,9 +45,10 @@ def _chk_frag(W: torch.Tensor, epi: int):
 def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_BF16,
          bias: Optional[torch.Tensor] = None, ksplit: int = 1, N: Optional[int] = None,
          aux: Optional[torch.Tensor] = None, aux_rows: int = 0, aux_out: Optional[torch.Tensor] = None,
-         aux_ld: int = 0, aux_n: int = 0, M: Optional[int] = None) -> torch.Tensor:
+         aux_ld: int = 0, aux_n: int = 0, M: Optional[int] = None, split_m: Optional[int] = None) -> torch.Tensor:
     """out = epilogue(A[M][K] . W[N][K]^T).  K = W.shape[1] (zero-padded), A.shape[1] >= K.
-    epi may carry W_FRAG (W fragment-packed, weights.frag_pack)."""
+    epi may carry W_FRAG (W fragment-packed, weights.frag_pack).  split_m: choose the small-M split-K of a bf16
+    epilogue as for that many rows (a data-parallel rank slice then sums in the same order as the whole batch)."""
     _chk(A, torch.bfloat16, "A")
     _chk(W, torch.bfloat16, "W")
     _chk_frag(W, epi)
@@ -73,7 +74,7 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
         _chk(out, torch.bfloat16, "out")
     if M > 16 and K % 64:
         raise ValueError("pghip.gemm: K must be a multiple of 64 for M > 16")
-    s = finalize_split(M, N, K) if ksplit == 1 and epi in _FIN_EPIS else 1
+    s = finalize_split(split_m or M, N, K) if ksplit == 1 and epi in _FIN_EPIS else 1
     if s > 1:   # small-M prefill: split K into fp32 slabs, then the epilogue in pg_gemm_finalize
         part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)
         _lib.call("pg_gemm", _p(A), A.stride(0), _p(W), W.stride(0), _p(bias), _p(part), N, M, N, K,

@@ -20,22 +20,24 @@ def _tiny_oracle(recompute=True, name="tiny"):
     return O.PaliGemmaOracle(cfg, synth.generate_state_dict(cfg), recompute_vision=recompute)
 
 
-@pytest.mark.parametrize("name,B", [("tiny", 1), ("tiny", 2), ("tiny8", 1), ("tiny8", 8)])
+@pytest.mark.parametrize("name,B", [("tiny", 1), ("tiny", 2), ("tiny8", 1), ("tiny8", 16)])
 def test_tiny_prefill_matches_reference(golden, name, B):
-    """tiny (4 q heads) and tiny8 (8 q heads, the tensor-parallel toy: B = 8 is one image per rank at TP=8)."""
+    """tiny (4 q heads) and tiny8 (8 q heads, the tensor-parallel toy: B = 16 is two images per rank at TP=8)."""
     g = golden(name)
     p = f"b{B}_"
     orc = _tiny_oracle(name=name)
     feats = orc.image_features(g[p + "pixel_values"])
-    v = O.siglip_vision_model(orc.W, orc.vcfg, g[p + "pixel_values"])
-    close(v, g[p + "vision_out"])
     close(feats, g[p + "proj_out"])
     kv = O.KVCache()
     taps = []
     res = orc.forward(g[p + "input_ids"], g[p + "pixel_values"], np.ones_like(g[p + "input_ids"]), kv, taps=taps)
+    close(res["logits"], g[p + "logits"])
+    if B > 2:                   # large toy batches keep inputs, logits and projector output only
+        return
+    v = O.siglip_vision_model(orc.W, orc.vcfg, g[p + "pixel_values"])
+    close(v, g[p + "vision_out"])
     for i, h in enumerate(taps):
         close(h, g[p + f"text_layer_{i}"])
-    close(res["logits"], g[p + "logits"])
     close(kv.k_cache[0], g[p + "k_cache0"])
     close(kv.v_cache[-1], g[p + "v_cache0"])
 

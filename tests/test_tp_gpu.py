@@ -76,22 +76,31 @@ def test_tp_engine_on_one_device(tmp_path, cfg, world, comm, chunk, fp8):
     if fp8:
         env["TP_FP8"] = "1"
     res = _launch("tp_worker.py", tmp_path, nproc=world, **env)
-    tol = 0.12 if fp8 else 3e-2                  # vs the fp32 reference (tests/test_engine_gpu.py)
+    print(json.dumps(res[0]))
     for o in res:
         assert o["xgmi_err"] == 0, o
         assert o["graph"] == (comm == "xgmi"), o
         assert o["world"] == world and (chunk is None or o["chunk_rows"] == chunk), o
-        pre = [k for k in o if k.startswith("prefill_err_b")]
-        assert pre and all(o[k] < tol for k in pre), o
-        assert all(o[k] < (tol if fp8 else 1e-2) for k in o if k.startswith("prefill_err_vs_solo")), o
+        # vs the fp32 reference: within 1.5x the model's intrinsic sensitivity to the path's operand rounding (the
+        # oracle run with bf16 operands, and e4m3 Gemma linears for fp8), as the full-size tests bound it
+        pre = [int(k[len("prefill_err_b"):]) for k in o if k.startswith("prefill_err_b")]
+        assert pre and all(o[f"prefill_err_b{B}"] < 1.5 * o[f"intrinsic_b{B}"] for B in pre), o
+        # vs the single-rank engine: other fp32 summation orders of the rank partials (bf16); fp8 ranks quantise
+        # other weight slices (o / down rows over a K slice get their own scales), so the fp8 bound applies
+        for B in pre:
+            assert o[f"prefill_err_vs_solo_b{B}"] < (1.5 * o[f"intrinsic_b{B}"] if fp8 else 5e-3), (B, o)
+        # the data-parallel SigLIP slice takes the whole batch's split choices: bit-identical features once a rank's
+        # slice is a tile GEMM (> 16 rows; a slice of <= 16 rows runs the decode GEMV, another summation order)
+        assert all(o[f"vision_dp_bitexact_b{B}"] for B in o["vision_dp"] if B // world * 16 > 16), o
         if cfg == "tiny8" and world == 8:
-            assert 8 in o["vision_dp"], o             # one image per rank through the data-parallel SigLIP
+            assert 16 in o["vision_dp"], o            # two images per rank through the data-parallel SigLIP
+        tol = 1.5 * max(o[f"intrinsic_b{B}"] for B in pre)
         if fp8:
             assert o["decode_slice_err"] < tol, o
-            assert o["fp8_decode24_err"] < tol, o
+            assert o["fp8_decode24_err"] < 1.5 * o["fp8_decode24_intrinsic"], o
         else:
             assert o["greedy"] == o["greedy_ref"], o
-            assert o["decode_slice_err"] < 5e-3, o
+            assert o["decode_slice_err"] < 0.5 * o["intrinsic_b1"], o      # fp32 order, bf16-amplified
             assert o["decode_argmax_agree"], o
             assert o["sampled_tp"] == o["sampled_solo"], o
     assert all(o["greedy"] == res[0]["greedy"] and o["sampled_tp"] == res[0]["sampled_tp"] for o in res)

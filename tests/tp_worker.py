@@ -67,6 +67,7 @@ def tiny(rank, world, name):
     issued asynchronously -- on the xGMI side stream or as an async gloo op -- while chunk c+1's GEMM runs).
     TP_FP8=1 packs fp8 Gemma linears (every linear of more than 16 rows runs on the block-scaled fp8 MFMA) and adds a
     24-row teacher-forced decode (fp8 decode path) against the oracle."""
+    import contextlib
     from pghip import configs, engine, synthetic, weights
     from pghip.tp import TPComm, XgmiComm
     from oracle import configs as ocfg, synth
@@ -83,22 +84,33 @@ def tiny(rank, world, name):
     g = dict(np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz")))
     out = {"rank": rank, "world": world, "comm": type(comm).__name__, "graph": comm.capturable, "cfg": name,
            "fp8": fp8, "chunk_rows": tp.AR_CHUNK_ROWS, "vision_dp": []}
+    ocfg_ = ocfg.CONFIGS[name]
+    W = synth.generate_state_dict(ocfg_)
     for B in sorted(int(k[1:-len("_logits")]) for k in g if k.startswith("b") and k.endswith("_logits")):
         p = f"b{B}_"
         ids = torch.from_numpy(g[p + "input_ids"]).cuda()
         px = torch.from_numpy(g[p + "pixel_values"]).cuda()
         Bv, L = ids.shape
-        lg = []
+        lg, fts = [], []
         for e in (tp, solo):
             cache = e.new_cache(Bv, L + 8)
             resid = torch.empty(Bv * L, e.w.hidden, device="cuda")
-            e.embed_merge(ids, e.vision(px), resid)
+            fts.append(e.vision(px))
+            e.embed_merge(ids, fts[-1], resid)
             pos = torch.arange(1, L + 1, dtype=torch.int32).repeat(Bv, 1)
             lg.append(e.gemma_prefill(resid, pos, cache, Bv, L)[0].clone())
         out[f"prefill_err_b{B}"] = err(lg[0].cpu().numpy(), g[p + "logits"].reshape(Bv * L, -1))
         out[f"prefill_err_vs_solo_b{B}"] = err(lg[0].cpu().numpy(), lg[1].cpu().numpy())
+        # the model's own sensitivity to the HIP path's operand rounding: the fp32 oracle with bf16 operands (and
+        # e4m3 Gemma linears of more than 16 rows for fp8) against the reference's logits
+        with O.bf16_operands(), (O.fp8_operands() if fp8 else contextlib.nullcontext()):
+            lo = O.PaliGemmaOracle(ocfg_, W, recompute_vision=False).forward(
+                g[p + "input_ids"], g[p + "pixel_values"], np.ones_like(g[p + "input_ids"]), O.KVCache())["logits"]
+        out[f"intrinsic_b{B}"] = err(lo.reshape(Bv * L, -1), g[p + "logits"].reshape(Bv * L, -1))
         if Bv >= world and Bv % world == 0:
             out["vision_dp"].append(B)
+            # data-parallel SigLIP with the whole batch's split choices: the same features as one rank, bit for bit
+            out[f"vision_dp_bitexact_b{B}"] = bool(torch.equal(fts[0], fts[1]))
     ids = torch.from_numpy(g["b1_input_ids"]).cuda()
     px = torch.from_numpy(g["b1_pixel_values"]).cuda()
     am = torch.ones_like(ids)
@@ -134,10 +146,10 @@ def tiny(rank, world, name):
     out["sampled_solo"] = solo.generate(ids, px, am, 8, do_sample=True, temperature=0.8, top_p=0.9, uniforms=u,
                                         stop_token=None)[0].tolist()
     if fp8:
-        # 24 rows (> 16: the fp8 decode path) of 24 different images, teacher-forced 3 steps, against the fp32 oracle
-        # (TP and single rank quantise different weight slices, so each is held to the fp8 bound on its own)
-        ocfg_ = ocfg.CONFIGS[name]
-        orc = O.PaliGemmaOracle(ocfg_, synth.generate_state_dict(ocfg_), recompute_vision=False)
+        # 24 rows (> 16: the fp8 decode path) of 24 different images, teacher-forced 3 steps, against the fp32 oracle,
+        # bounded by the oracle's own fp8-operand emulation of the same rows (every Gemma linear fp8)
+        orc = O.PaliGemmaOracle(ocfg_, W, recompute_vision=False)
+        emu = O.PaliGemmaOracle(ocfg_, W, recompute_vision=False)
         Bd, size = 24, ocfg_["vision_config"]["image_size"]
         rng = np.random.default_rng(11)
         pxb = rng.standard_normal((Bd, 3, size, size)).astype(np.float32)
@@ -148,8 +160,15 @@ def tiny(rank, world, name):
         s_ = tp.decode_state(Bd, c, n, 4)
         samp = dict(do_sample=True, temperature=0.8, top_p=0.9, uniforms=torch.full((5, Bd), 0.5, device="cuda"))
         kvs = [O.KVCache() for _ in range(Bd)]
+        kve = [O.KVCache() for _ in range(Bd)]
+
+        def emu_fwd(*a, **k):
+            with O.bf16_operands(), O.fp8_operands(min_rows=0):
+                return emu.forward(*a, **k)
         ref = [orc.forward(ids_b[b:b + 1], pxb[b:b + 1], amb[b:b + 1], kvs[b], logits_rows=slice(-1, None))
                ["logits"][0, -1] for b in range(Bd)]
+        ie = [err(emu_fwd(ids_b[b:b + 1], pxb[b:b + 1], amb[b:b + 1], kve[b], logits_rows=slice(-1, None))
+                  ["logits"][0, -1], ref[b]) for b in range(Bd)]
         fe = [err(lg0[b].cpu().numpy(), ref[b]) for b in range(Bd)]
         for t in range(3):
             tok = [5 + (7 * b + 11 * t) % 250 for b in range(Bd)]         # ordinary text ids (no image / pad id)
@@ -161,7 +180,10 @@ def tiny(rank, world, name):
                 r = orc.forward(np.array([[tok[b]]]), pxb[b:b + 1], np.ones((1, L1), np.int64), kvs[b],
                                 logits_rows=slice(-1, None))["logits"][0, -1]
                 fe.append(err(lgd[b], r))
+                ie.append(err(emu_fwd(np.array([[tok[b]]]), pxb[b:b + 1], np.ones((1, L1), np.int64), kve[b],
+                                      logits_rows=slice(-1, None))["logits"][0, -1], r))
         out["fp8_decode24_err"] = max(fe)
+        out["fp8_decode24_intrinsic"] = max(ie)
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
     if isinstance(comm, XgmiComm):
