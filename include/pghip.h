@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 8: pg_allreduce_xgmi_slabs; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -39,9 +39,12 @@ enum {
   PG_EPI_BF16_VT = 5,       /* cols < aux_n -> C bf16; cols >= aux_n -> aux_out[(n-aux_n)*aux_ld + m] */
   PG_EPI_QKV_ROPE = 6,      /* fused q|k|v (rope-permuted W rows): RoPE(q) -> C, RoPE(k) -> K cache, v -> V^T
                                cache (gemma.py:274-302 + KVCache.update :18-57); pg_gemm_fused only          */
-  PG_EPI_F32_FIN = 7        /* M <= 4: F32 slabs, then the last split of each 16-column tile adds them into
+  PG_EPI_F32_FIN = 7,       /* M <= 4: F32 slabs, then the last split of each 16-column tile adds them into
                                fin_resid and writes ss_out (the residual add of gemma.py:401,416 + the next
                                RMSNorm's sum of squares); pg_gemm_fused only                                  */
+  PG_EPI_F32_ADD = 8        /* (ABI 8) M <= 16, pro_mode 0 or 2: C f32 [M][ldc] += acc (+ bias by split 0) by
+                               hardware float atomic adds in any split order (the residual add of gemma.py:401,416
+                               with no slab or ticket; the next GEMV normalises with pro_mode 1, nsplit 0)       */
 };
 
 /* Fused-operation arguments of pg_gemm_fused (M <= 16 for the prologues). */

@@ -42,6 +42,8 @@ enum {
   PG_EPI_F32_FIN = 7,       // GEMV (M <= 16) split-K slabs as PG_EPI_F32, then the last-arriving split of each
                             // output tile adds the slabs into fin_resid and writes the tile's sum of squares
                             // (ss_out): the residual add + RMSNorm statistics of the NEXT norm, done in-kernel
+  PG_EPI_F32_ADD = 8,       // GEMV (M <= 16): C f32 [M][ldc] += acc (+ bias by split 0) with hardware float atomic
+                            // adds, any split count (the residual add of a row-parallel decode linear, no slabs)
 };
 
 // Extra arguments of the fused entry point pg_gemm_fused (mirrors PgFusedArgs in include/pghip.h).
@@ -1304,6 +1306,25 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
+  if constexpr (EPI == PG_EPI_F32_ADD) {
+    // C[m][n] += acc (+ bias by split 0): hardware float atomic adds at the memory side, no slab, no ticket --
+    // the launch ends one atomic round trip after its last MFMA (the F32_FIN tail is slab store -> ticket -> slab
+    // load).  The split order of the adds is unordered (fp32 rounding of the sum may differ run to run).
+    if (m < M) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n0 = (tile0 + t) * 16 + q;
+        if (n0 < e.N) {
+          f32x4 v = acc[t];
+          if (e.bias && z == 0) v += load4_guard(e.bias, n0, e.N);
+          float* dst = (float*)e.C + (size_t)m * e.ldc + n0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) unsafeAtomicAdd(dst + j, v[j]);
+        }
+      }
+    }
+    return;
+  }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
     epi_gelu_mul4(e, m, tile0 * 16, q, acc[0], acc[1]);
   } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
@@ -1509,6 +1530,13 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
 template <int EPI, bool FRAG>
 static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
+  if constexpr (EPI == PG_EPI_F32_ADD) {     // (plain x, or the attention merge: o_proj / down_proj)
+    if (e.f.pro_mode == 2)
+      launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+    else
+      launch_gemv_pro<EPI, 0, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
+    return;
+  }
   switch (e.f.pro_mode) {
     case 1: launch_gemv_pro<EPI, 1, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
     case 2: launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st); break;
@@ -1524,7 +1552,7 @@ static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K
                        hipStream_t st, bool m1 = false, bool n64 = false) {
   if (e.M <= 16)
     launch_gemv<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
-  else if constexpr (EPI != PG_EPI_F32_FIN)
+  else if constexpr (EPI != PG_EPI_F32_FIN && EPI != PG_EPI_F32_ADD)
     launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st, m1, n64);
 }
 
@@ -1543,7 +1571,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
                        (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||
-                        epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN));
+                        epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD));
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
@@ -1565,7 +1593,8 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                   f.ss_ld >= f.ss_n && K % 4 == 0);
   if (epi == PG_EPI_F32_FIN) PG_REQUIRE(M <= 16 && ksplit <= 8 && (f.fin_x == nullptr || f.norm_w != nullptr) && f.fin_cnt && f.fin_resid && f.ss_out && f.ss_ld >= (N + 15) / 16 &&
                                         ldc == N);
-  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN);
+  if (epi == PG_EPI_F32_ADD) PG_REQUIRE(M <= 16 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N);
+  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
   if (epi == PG_EPI_BF16_VT) PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
@@ -1604,6 +1633,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
     PG_CASE(PG_EPI_F32)
     PG_CASE(PG_EPI_QKV_ROPE)
     PG_CASE(PG_EPI_F32_FIN)
+    PG_CASE(PG_EPI_F32_ADD)
     PG_CASE_ROWMAJOR(PG_EPI_BF16_GELU)
     PG_CASE_ROWMAJOR(PG_EPI_F32_POS)
     PG_CASE_ROWMAJOR(PG_EPI_BF16_VT)

@@ -132,6 +132,11 @@ class PaliGemmaEngine:
     # fp8 decode (> 16 rows): the one-launch attention also writes its rows as e4m3 for the fp8 o_proj (no
     # pg_quant_fp8 launch; same bytes)
     ATTN_FP8_OUT = os.environ.get("PG_ATTN_FP8_OUT", "1") != "0"
+    # B <= FUSE_MAX_B single rank: row-parallel decode linears that add their split-K partials straight into the
+    # residual with float atomics (PG_EPI_F32_ADD) instead of finalising slabs in-kernel (F32_FIN's slab store ->
+    # ticket -> slab load tail); the next GEMV then normalises the residual itself (PRO_RMSNORM).  "down": down_proj
+    # of every layer but the last (whose FIN output feeds the lm_head); "both": o_proj too; "0": off
+    DECODE_ADD = os.environ.get("PG_DECODE_ADD", "both")
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -687,11 +692,13 @@ class PaliGemmaEngine:
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
         SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
+        add_down = merge_in_gemv and self.DECODE_ADD in ("down", "both")
+        add_o = merge_in_gemv and self.DECODE_ADD == "both"
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                         q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
-            if i == 0:      # the embedding rows are final: plain RMSNorm prologue
+            if i == 0 or add_down:  # the residual rows are final (embedding, or atomically added): RMSNorm prologue
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
                                     **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
@@ -704,26 +711,41 @@ class PaliGemmaEngine:
                               B=B, Lq=1, Lkv=1, lkv_dev=st["kv_len"], Hq=nh, Hkv=nkv, D=hd,
                               scale=1.0 / math.sqrt(hd), split_keys=SK, nsplit=nsplit, part_o=part_o,
                               part_ml=part_ml, kcap=cache.Smax, kd=cache.kd[i], vd=cache.vd[i])
-                fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
-                                    head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
-                                    akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
-                                    norm_w=Lw["post_w"])
-                ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
+                if add_o:
+                    fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                        head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
+                                        akeys=SK)
+                    ops.gemm_fused(None, Lw["o_w"], res, fa, epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=so)
+                else:
+                    fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
+                                        head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
+                                        akeys=SK, fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
+                                        norm_w=Lw["post_w"])
+                    ops.gemm_fused(None, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             else:
                 self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK, nsplit)
                 fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_o, ss_ld=tiles, fin_x=xq,
                                     norm_w=Lw["post_w"])
                 ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
-            self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd)
+            self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd,
+                          add=add_down and i + 1 < nl, gu_rms=add_o)
         return xq, ss_d, tiles, n_ss
 
-    def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd):
+    def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd, add=False, gu_rms=False):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
-        (x' of the next norm -> xq, its sums of squares -> ss_d)."""
+        (x' of the next norm -> xq, its sums of squares -> ss_d).  add: down adds its partials into res with float
+        atomics (EPI_F32_ADD; the next GEMV normalises res itself).  gu_rms: o_proj did so, gate/up normalises res."""
         w = self.w
-        fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
-        ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+        if gu_rms:
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["post_w"], eps=1e-6)
+            ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+        else:
+            fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
+            ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
+        if add:
+            ops.gemm_fused(h, Lw["down_w"], res, ops.fused_args(), epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=sd)
+            return
         fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
         ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
 

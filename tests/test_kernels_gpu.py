@@ -679,6 +679,27 @@ def test_gemm_fused_attention_merge_prologue(B):
     assert err(ref_o, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M,z,frag", [(1, 1, True), (1, 8, True), (2, 2, True), (5, 4, False), (16, 3, True)])
+def test_gemm_f32_add_epilogue_residual_accumulates(M, z, frag):
+    """PG_EPI_F32_ADD: the GEMV adds its split-K partials (+ bias, once) into the residual with float atomics:
+    resid += x . W^T, equal to the fp32 reference up to the fp32 order of the split sums; rows past M untouched;
+    with the attention-merge prologue (o_proj) as well."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    K, N = 2048, 1024
+    x = rnd(M, K, seed=31)
+    W = rnd(N, K, scale=1 / 45, seed=32)
+    bias = torch.randn(N).cuda() * 0.1
+    resid = torch.randn(M + 1, N).cuda()
+    r0 = resid.clone()
+    Wk = frag_pack(W) if frag else W
+    ops.gemm_fused(x, Wk, resid, ops.fused_args(), epi=ops.EPI_F32_ADD | (ops.W_FRAG if frag else 0), M=M, ksplit=z,
+                   bias=bias)
+    ref = r0[:M] + x.float() @ W.float().t() + bias
+    assert err(resid[:M], ref) < 1e-5
+    assert torch.equal(resid[M:], r0[M:])
+
+
 @pytest.mark.parametrize("M,L,H", [(1, 1, 512), (3, 1, 512), (40, 20, 512), (264, 264, 512), (264, 264, 2048)])
 def test_gemm_fused_qkv_rope_epilogue(M, L, H):
     """q|k|v GEMM with RoPE + KV append in the epilogue == plain GEMM + pg_rope_kv_write (H = 2048 at M = 264:
