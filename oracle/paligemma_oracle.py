@@ -52,20 +52,23 @@ class bf16_operands:
 # each scaled by max|row| / 448 (weights.quant_rows_fp8 / pg_quant_fp8's rule) -- whenever a call has more than
 # `min_rows` rows (the HIP path runs fp8 for linears of more than 16 rows: prefill, and decode at batch > 16).
 # The fp8 path's intrinsic sensitivity on a model then bounds the HIP fp8 path's distance to the fp32 reference.
+# lm_head=True also runs the tied lm_head on e4m3 operands (the HIP path's batch > 16 decode lm_head).
 _FP8_MIN_ROWS = None
+_FP8_LM_HEAD = False
 
 
 class fp8_operands:
-    def __init__(self, min_rows: int = 16):
-        self.min_rows = min_rows
+    def __init__(self, min_rows: int = 16, lm_head: bool = False):
+        self.min_rows, self.lm_head = min_rows, lm_head
 
     def __enter__(self):
-        global _FP8_MIN_ROWS
-        self._old, _FP8_MIN_ROWS = _FP8_MIN_ROWS, self.min_rows
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD
+        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD)
+        _FP8_MIN_ROWS, _FP8_LM_HEAD = self.min_rows, self.lm_head
 
     def __exit__(self, *a):
-        global _FP8_MIN_ROWS
-        _FP8_MIN_ROWS = self._old
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD
+        _FP8_MIN_ROWS, _FP8_LM_HEAD = self._old
 
 
 def q8_rows(x: np.ndarray) -> np.ndarray:
@@ -313,7 +316,7 @@ def gemma_for_causal_lm(W: dict, tcfg: dict, input_embeds, position_ids, mask, k
     if logits_rows is not None:
         h = h[:, logits_rows]
     emb = W["language_model.model.embed_tokens.weight"]                 # tied (:492-499)
-    return linear(h, emb, W["language_model.lm_head.bias"])             # :523-525
+    return linear(h, emb, W["language_model.lm_head.bias"], gemma=_FP8_LM_HEAD)   # :523-525
 
 
 # --------------------------------------------------------------------------- #

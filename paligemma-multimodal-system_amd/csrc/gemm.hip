@@ -260,6 +260,16 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x
   }
 }
 
+// C[m][n0..n0+3] += v (+ bias by split 0) with hardware float atomic adds (PG_EPI_F32_ADD; unordered over splits)
+__device__ __forceinline__ void epi_add4(const EpiArgs& e, int m, int n0, f32x4 v, int z) {
+  if (m >= e.M || n0 >= e.N) return;
+  if (e.bias && z == 0) v += load4_guard(e.bias, n0, e.N);
+  float* dst = (float*)e.C + (size_t)m * e.ldc + n0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (n0 + j < e.N) unsafeAtomicAdd(dst + j, v[j]);
+}
+
 // gelu(gate) * up for an interleaved pair: gate tile at global col base gb (multiple of 32),
 // lane's 4 columns are gb + q..q+3 (gate) and gb + 16 + q.. (up); output col = gb/2 + q.
 __device__ __forceinline__ void epi_gelu_mul4(const EpiArgs& e, int m, int gb, int q, f32x4 g, f32x4 u) {
@@ -1352,6 +1362,323 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 }
 
 // --------------------------------------------------------------------------------------
+// fp8 weight-streaming GEMV for 17..32 rows (batched decode on the fp8 path, BASELINE configs[4])
+// --------------------------------------------------------------------------------------
+// The batch-32 decode linears read each e4m3 weight once per step; as 64 x 128 / 128 x 128 tile GEMMs they staged
+// W through LDS at 3.1-3.3 TB/s.  Here, as in gemv_body, W streams straight to VGPRs: the weights are stored
+// fragment-packed (PG_W_FRAG with PG_FP8, weights.frag_pack8): W[16t + r][128c + 64s + 16g + e] (e < 16 bytes) at
+// byte ((t * (K/128) + c) * 2 + s) * 1024 + (16g + r) * 16 + e, so piece s of a 16-row x 128-k chunk is one 1-KiB
+// lane-linear non-temporal load.  Lane (r, g) loads x row r (and 16 + r) at the same k bytes, one
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per (W tile, 16-row x tile) and chunk; the 4 waves split
+// the chunks of split blockIdx.y round-robin, DEPTH chunks in flight, and reduce through LDS.  The accumulator is
+// scaled by a_scale[m] * w_scale[n] before the tile kernel's epilogues (bf16, gelu*up, fp32 slabs, RoPE + KV).
+template <int EPI, int NT, int MT, int DEPTH, int CPW>
+__global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ X, int ldx,
+                                                    const uint8_t* __restrict__ W, int K, EpiArgs e) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int tile0 = blockIdx.x * NT;
+  const int M = e.M;
+  const int z = blockIdx.y;
+  const int nch_all = K >> 7;
+  const int per_z = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = z * per_z;
+  const int nch = min(nch_all - c0, per_z);
+  const int mine = CPW > 0 ? CPW : (nch > wave ? (nch - wave + 3) / 4 : 0);   // chunks wave, wave + 4, ...
+  const uint8_t* wt[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) wt[t] = W + (size_t)min(tile0 + t, (e.N >> 4) - 1) * 16 * K + lane * 16;
+  const uint8_t* xr[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) xr[mt] = X + (size_t)min(mt * 16 + r, M - 1) * ldx + g * 16;
+  f32x4 acc[NT][MT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 wb[DEPTH][NT][2], xb[DEPTH][MT][2];
+  auto load = [&](int j, u32x4 (&wv)[NT][2], u32x4 (&xv)[MT][2]) {
+    const size_t cc = (size_t)(c0 + wave + j * 4);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+        wv[t][sp] = __builtin_nontemporal_load((const u32x4*)(wt[t] + (cc * 2 + sp) * 1024));
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) xv[mt][sp] = *(const u32x4*)(xr[mt] + cc * 128 + sp * 64);
+  };
+  auto compute = [&](const u32x4 (&wv)[NT][2], const u32x4 (&xv)[MT][2]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]),
+                           __builtin_bit_cast(bf16x8, xv[mt][0]), __builtin_bit_cast(bf16x8, xv[mt][1]), acc[t][mt]);
+  };
+  // (QKV epilogue operands issued with the stream, as gemv_body does, are not needed: the tile epilogue loads them)
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (CPW > 0 ? d < CPW : d < mine) load(d, wb[d], xb[d]);
+  if constexpr (CPW > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int d = j % DEPTH;
+      compute(wb[d], xb[d]);
+      if (j + DEPTH < CPW) load(j + DEPTH, wb[d], xb[d]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    for (int base = 0; base < mine; base += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        const int j = base + d;
+        if (j < mine) {
+          compute(wb[d], xb[d]);
+          if (j + DEPTH < mine) load(j + DEPTH, wb[d], xb[d]);
+        }
+      }
+    }
+  }
+  __shared__ f32x4 red[4][NT][MT][64];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wave][t][mt][lane] = acc[t][mt];
+  __syncthreads();
+  if (wave != 0) return;
+  const int q = 4 * g;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + r;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      acc[t][mt] = red[0][t][mt][lane] + red[1][t][mt][lane] + red[2][t][mt][lane] + red[3][t][mt][lane];
+      scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+    }
+    if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+#pragma unroll
+      for (int t = 0; t < NT; t += 2) epi_gelu_mul4(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]);
+    } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) epi_qkv_rope4(e, m, (tile0 + t) * 16 + q, acc[t][mt]);   // (all lanes: shuffle)
+    } else if constexpr (EPI == PG_EPI_F32_ADD) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) epi_add4(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    }
+  }
+}
+
+// The wide form (large N: gate/up, down, the lm_head): x is staged ONCE per workgroup in LDS and the 4 waves split
+// the W tiles instead of K (wave w owns tiles tile0 + w*NTW ...), so a workgroup reads x[32][Kr] once for 4 * NTW
+// tiles -- at 32 rows x costs as many bytes per 16-row tile as the tile itself, and the per-CU load rate, not HBM,
+// bounded the K-split form (gate/up 4.3 TB/s, down 2.9).  x [M <= 32][Kr] arrives by LDS-DMA (1 KiB pieces, the 16-B
+// chunks of a row XOR-swizzled by row through the source address), issued before the W stream; each wave then
+// streams its own W tiles DEPTH chunks deep and reads its x fragments from LDS.  No cross-wave reduction: every
+// wave runs the epilogue of its own tiles (bf16, gelu*up on gate/up pairs, fp32 slabs, float-atomic residual add).
+template <int EPI, int NTW, int MT, int DEPTH, int CPW>
+__global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__ X, int ldx,
+                                                     const uint8_t* __restrict__ W, int K, EpiArgs e) {
+  extern __shared__ __attribute__((aligned(16))) char xs8[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int tile0 = (blockIdx.x * 4 + wave) * NTW;
+  const int M = e.M;
+  const int z = blockIdx.y;
+  const int nch_all = K >> 7;
+  const int per_z = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int c0 = z * per_z;
+  const int nch = CPW > 0 ? CPW : max(0, min(nch_all - c0, per_z));
+  const int Kr = nch * 128;                        // bytes of one x row in LDS
+  // 1. x rows [0, 16 MT) x bytes [128 c0, +Kr) into LDS by DMA: LDS byte o = row * Kr + 16 pc holds logical chunk
+  //    pc ^ (row & 7) of the row (rows past M repeat row M-1: their outputs are never stored)
+  {
+    const int pieces = MT * 16 * Kr / 1024;        // 1 KiB each, dealt round-robin to the waves
+    for (int pi = wave; pi < pieces; pi += 4) {
+      const int o = pi * 1024 + lane * 16;
+      const int row = o / Kr, pc = (o % Kr) >> 4;
+      const int lc = pc ^ (row & 7);
+      const uint8_t* src = X + (size_t)min(row, M - 1) * ldx + (size_t)c0 * 128 + lc * 16;
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(xs8 + pi * 1024), 16, 0, 0);
+    }
+  }
+  const int my_pieces = (MT * 16 * Kr / 1024 - wave + 3) / 4;   // this wave's DMA pieces (vmcnt bookkeeping)
+  const uint8_t* wt[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) wt[t] = W + (size_t)min(tile0 + t, (e.N >> 4) - 1) * 16 * K + lane * 16;
+  f32x4 acc[NTW][MT];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  u32x4 wb[DEPTH][NTW][2];
+  auto loadw = [&](int j, u32x4 (&wv)[NTW][2]) {
+    const size_t cc = (size_t)(c0 + j);
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+        wv[t][sp] = __builtin_nontemporal_load((const u32x4*)(wt[t] + (cc * 2 + sp) * 1024));
+  };
+  // 2. the W stream, DEPTH chunks deep, issued behind the x pieces
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (CPW > 0 ? d < CPW : d < nch) loadw(d, wb[d]);
+  // 3. this wave's x pieces have landed once at most its W loads are outstanding; the barrier covers the others'
+  {
+    const int wl = (CPW > 0 ? min(DEPTH, CPW) : min(DEPTH, nch)) * NTW * 2;
+    (void)my_pieces;
+    wait_vm_n(wl);
+    __syncthreads();
+  }
+  auto compute = [&](int j, const u32x4 (&wv)[NTW][2]) {
+    bf16x8 xf[MT][2];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int row = mt * 16 + r;
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        const int lc = j * 8 + sp * 4 + g;
+        xf[mt][sp] = *(const bf16x8*)(xs8 + row * Kr + ((lc ^ (row & 7)) << 4));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
+                           xf[mt][1], acc[t][mt]);
+  };
+  if constexpr (CPW > 0) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int d = j % DEPTH;
+      compute(j, wb[d]);
+      if (j + DEPTH < CPW) loadw(j + DEPTH, wb[d]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    for (int base = 0; base < nch; base += DEPTH) {
+#pragma unroll
+      for (int d = 0; d < DEPTH; ++d) {
+        const int j = base + d;
+        if (j < nch) {
+          compute(j, wb[d]);
+          if (j + DEPTH < nch) loadw(j + DEPTH, wb[d]);
+        }
+      }
+    }
+  }
+  const int q = 4 * g;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + r;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+    if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+#pragma unroll
+      for (int t = 0; t < NTW; t += 2) epi_gelu_mul4(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]);
+    } else if constexpr (EPI == PG_EPI_F32_ADD) {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) epi_add4(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    }
+  }
+}
+
+template <int EPI, int NTW, int MT>
+static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
+                             hipStream_t st) {
+  const int tiles = e.N >> 4;
+  const dim3 grid((tiles + 4 * NTW - 1) / (4 * NTW), ksplit);
+  const int nch = K >> 7;
+  const int per_z = (nch + ksplit - 1) / ksplit;
+  const size_t lds = (size_t)MT * 16 * per_z * 128;
+  const bool exact = nch % ksplit == 0;
+  if (exact && per_z == 16)
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+  else if (exact && per_z == 8)
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 8>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+  else
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 0>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+}
+
+#ifndef PG_GEMV8_DEPTH
+#define PG_GEMV8_DEPTH 4
+#endif
+template <int EPI, int NT, int MT>
+static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
+                            hipStream_t st) {
+  const dim3 grid(((e.N >> 4) + NT - 1) / NT, ksplit);
+  const int nch = K >> 7;
+  const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
+  constexpr int D = PG_GEMV8_DEPTH;                // chunks in flight per wave
+  switch (cpw) {
+    case 2: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, 2, 2>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 4: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 4>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 8: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 8>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    default: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 0>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+  }
+}
+
+template <int EPI, int NT>
+static void launch_gemv8_nt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
+                            hipStream_t st) {
+  if (e.M <= 16)
+    launch_gemv8_mt<EPI, NT, 1>(X, ldx, W, K, ksplit, e, st);
+  else
+    launch_gemv8_mt<EPI, NT, 2>(X, ldx, W, K, ksplit, e, st);
+}
+
+#ifndef PG_GEMV8_NT_MAX
+#define PG_GEMV8_NT_MAX 4
+#endif
+// NT W tiles per workgroup: every lane loads the x rows of its chunks once per workgroup, as many bytes per 16-row W
+// tile as the tile itself at 32 rows, so wide tiles amortise x -- the most tiles per workgroup that still leave
+// >= 256 workgroups (gelu*up: whole gate/up pairs); MT = 16-row x tiles
+#ifndef PG_GEMV8_WIDE
+#define PG_GEMV8_WIDE 1
+#endif
+template <int EPI>
+static void launch_gemv8(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
+                         hipStream_t st) {
+  const int tiles = e.N >> 4;
+  // the wide form (x once per workgroup in LDS, waves split N) when its grid still has >= 256 workgroups and a
+  // split's x rows fit the LDS; the K-split form otherwise (q|k|v: 160 tiles; o_proj)
+  const int per_z = ((K >> 7) + ksplit - 1) / ksplit;
+  if constexpr (EPI != PG_EPI_QKV_ROPE) {
+    if (PG_GEMV8_WIDE && per_z * 128 <= 4096) {
+      const int wgs2 = (tiles + 7) / 8 * ksplit, wgs1 = (tiles + 3) / 4 * ksplit;
+      if (e.M <= 16) {
+        if (wgs2 >= 256 || EPI == PG_EPI_BF16_GELU_MUL) { launch_gemv8x_mt<EPI, 2, 1>(X, ldx, W, K, ksplit, e, st); return; }
+        if constexpr (EPI != PG_EPI_BF16_GELU_MUL)
+          if (wgs1 >= 256) { launch_gemv8x_mt<EPI, 1, 1>(X, ldx, W, K, ksplit, e, st); return; }
+      } else {
+        if (wgs2 >= 256 || EPI == PG_EPI_BF16_GELU_MUL) { launch_gemv8x_mt<EPI, 2, 2>(X, ldx, W, K, ksplit, e, st); return; }
+        if constexpr (EPI != PG_EPI_BF16_GELU_MUL)
+          if (wgs1 >= 256) { launch_gemv8x_mt<EPI, 1, 2>(X, ldx, W, K, ksplit, e, st); return; }
+      }
+    }
+  }
+  if (PG_GEMV8_NT_MAX >= 4 && tiles % 4 == 0 && (tiles / 4) * ksplit >= 256)
+    launch_gemv8_nt<EPI, 4>(X, ldx, W, K, ksplit, e, st);
+  else if (EPI == PG_EPI_BF16_GELU_MUL || (PG_GEMV8_NT_MAX >= 2 && tiles % 2 == 0 && (tiles / 2) * ksplit >= 256))
+    launch_gemv8_nt<EPI, 2>(X, ldx, W, K, ksplit, e, st);
+  else if constexpr (EPI != PG_EPI_BF16_GELU_MUL)
+    launch_gemv8_nt<EPI, 1>(X, ldx, W, K, ksplit, e, st);
+}
+
+// --------------------------------------------------------------------------------------
 // Split-K finalisation for the bf16 epilogues (prefill at small M, where a full-K tile grid leaves CUs
 // idle): the GEMM writes fp32 slabs [z][M][N] (bias in slab 0), this kernel sums them and applies the
 // epilogue (bf16 / gelu / gelu*up / V^T side output / RoPE + KV-cache append).  One thread per 4 outputs.
@@ -1569,7 +1896,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (n64) PG_REQUIRE(M > 16);
   PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
-  if (frag) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
+  if (frag && !fp8) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
                        (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||
                         epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD));
   PgFusedArgs f{};
@@ -1593,7 +1920,8 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                   f.ss_ld >= f.ss_n && K % 4 == 0);
   if (epi == PG_EPI_F32_FIN) PG_REQUIRE(M <= 16 && ksplit <= 8 && (f.fin_x == nullptr || f.norm_w != nullptr) && f.fin_cnt && f.fin_resid && f.ss_out && f.ss_ld >= (N + 15) / 16 &&
                                         ldc == N);
-  if (epi == PG_EPI_F32_ADD) PG_REQUIRE(M <= 16 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N);
+  if (epi == PG_EPI_F32_ADD) PG_REQUIRE((M <= 16 || (fp8 && frag && M <= 32)) && (f.pro_mode == 0 || f.pro_mode == 2) &&
+                                        ldc >= N);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
@@ -1602,6 +1930,24 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   else PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0 && epi != PG_EPI_F32_FIN);
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
+  if (fp8 && frag) {
+    // fp8 weight-streaming GEMV (M <= 32): fp8 fragment-packed W (weights.frag_pack8), row-major e4m3 x
+    PG_REQUIRE(M <= 32 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && N % 16 == 0 && ldw == K &&
+               lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 &&
+               epi != PG_EPI_F32_FIN);
+    const uint8_t* x8 = (const uint8_t*)A;
+    const uint8_t* w8 = (const uint8_t*)W;
+    switch (epi) {
+      case PG_EPI_BF16: launch_gemv8<PG_EPI_BF16>(x8, lda, w8, K, ksplit, e, stream); break;
+      case PG_EPI_BF16_GELU_MUL: launch_gemv8<PG_EPI_BF16_GELU_MUL>(x8, lda, w8, K, ksplit, e, stream); break;
+      case PG_EPI_F32: launch_gemv8<PG_EPI_F32>(x8, lda, w8, K, ksplit, e, stream); break;
+      case PG_EPI_QKV_ROPE: launch_gemv8<PG_EPI_QKV_ROPE>(x8, lda, w8, K, ksplit, e, stream); break;
+      case PG_EPI_F32_ADD: launch_gemv8<PG_EPI_F32_ADD>(x8, lda, w8, K, ksplit, e, stream); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    PG_LAUNCH_CHECK();
+    return 0;
+  }
   if (fp8) {
     // fp8 e4m3 operands, tile GEMMs only; the kernels see byte pairs, so K / lda / ldw are halved
     PG_REQUIRE(!frag && M > 16 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && lda % 16 == 0 &&

@@ -137,6 +137,10 @@ class PaliGemmaEngine:
     # ticket -> slab load tail); the next GEMV then normalises the residual itself (PRO_RMSNORM).  "down": down_proj
     # of every layer but the last (whose FIN output feeds the lm_head); "both": o_proj too; "0": off
     DECODE_ADD = os.environ.get("PG_DECODE_ADD", "both")
+    # fp8 linears of 17..32 rows (batched decode, the lm_head of a 17..32-row batch) on the weight-streaming fp8 GEMV
+    # (fragment-packed e4m3 weights, csrc/gemm.hip gemv8_kernel) instead of the LDS-staged fp8 tile GEMM
+    FP8_GEMV = os.environ.get("PG_FP8_GEMV", "1") != "0"
+    DECODE_ADD_B32 = os.environ.get("PG_DECODE_ADD_B32", "0") == "1"   # (see _decode_layers_unfused)
 
     def __init__(self, cfg: dict, weights: PackedWeights, device="cuda", comm=None):
         self.cfg = cfg
@@ -367,14 +371,17 @@ class PaliGemmaEngine:
         """One Gemma linear: bf16 (fragment-packed W) or, with fp8 weights and M > 16, the activation rows
         quantised to e4m3 (pg_quant_fp8) feeding the PG_FP8 GEMM with the per-channel weight scales."""
         w = self.w
-        if isinstance(x, tuple):        # already quantised (_norm)
-            x8, xs = x
-            return ops.gemm8(x8, xs, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa)
-        if self._fp8_rows(M):
+        if not isinstance(x, tuple) and self._fp8_rows(M):
             K = x.shape[1]
             x8 = self._buf(f"x8_{K}", (M, K), torch.uint8)
             xs = self._buf(f"xs_{K}", (M,), torch.float32)
             ops.quant_fp8(x, x8, xs, M=M)
+            x = (x8, xs)
+        if isinstance(x, tuple):        # fp8 rows (quantised here, by _norm, or by the attention kernel)
+            x8, xs = x
+            if self.FP8_GEMV and M <= 32 and name + "_w8f" in Lw:
+                return ops.gemm8(x8, xs, Lw[name + "_w8f"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit,
+                                 fa=fa, frag=True)
             return ops.gemm8(x8, xs, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa)
         W, flag = Lw[name + "_w"], w.wflag
         if M >= self.PREFILL_ROWMAJOR_MIN_M and name + "_wr" in Lw:
@@ -498,16 +505,28 @@ class PaliGemmaEngine:
             (lambda shape: self._buf(name, shape, torch.float32))
         if self.tp == 1:
             logits = alloc((rows, w.vocab_local_pad))      # lm_w rows padded to 16 (fragment packing)
-            ops.gemm(xf, w.lm_w, logits, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
+            self._lm_gemm(xf, rows, logits)
             return logits[:, :w.vocab]
         vl, vlp = w.vocab_local, w.vocab_local_pad
         loc = self._buf(name + "_loc", (rows, vlp), torch.float32)
-        ops.gemm(xf, w.lm_w, loc, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
+        self._lm_gemm(xf, rows, loc)
         g = self._buf(name + "_gather", (self.tp, rows, vlp), torch.float32)
         self.comm.all_gather(g, loc)                                      # [rank][rows][vocab slice]
         out = alloc((rows, w.vocab))
         out.view(rows, self.tp, vl).copy_(g[:, :, :vl].permute(1, 0, 2))
         return out
+
+    def _lm_gemm(self, xf: torch.Tensor, rows: int, out: torch.Tensor):
+        """This rank's lm_head rows [rows][vocab_local_pad] fp32 (+ bias) from normalised bf16 rows: bf16 GEMV / GEMM,
+        or with fp8 weights at 17..32 rows the e4m3 rows through the fp8 GEMV (half the 1.05 GB of bf16 weights)."""
+        w = self.w
+        if self.FP8_GEMV and self._fp8_rows(rows) and rows <= 32 and getattr(w, "lm_w8f", None) is not None:
+            H = xf.shape[1]
+            x8 = self._buf(f"x8_{H}", (rows, H), torch.uint8)
+            xs = self._buf(f"xs_{H}", (rows,), torch.float32)
+            ops.quant_fp8(xf, x8, xs, M=rows)
+            return ops.gemm8(x8, xs, w.lm_w8f, w.lm_s8, out, epi=ops.EPI_F32, M=rows, bias=w.lm_bias, frag=True)
+        return ops.gemm(xf, w.lm_w, out, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
 
     # ------------------------------------------------------------------ decode step (graph-capturable)
     def _chain_ok(self, sampler) -> bool:
@@ -604,7 +623,7 @@ class PaliGemmaEngine:
         if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
             # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
             loc = self._buf("d_logits_loc", (B, w.vocab_local_pad), torch.float32)
-            ops.gemm(xn, w.lm_w, loc, epi=ops.EPI_F32 | w.wflag, bias=w.lm_bias)
+            self._lm_gemm(xn, B, loc)
             loc = loc[:, :w.vocab_local]
             Bp = B + (B & 1)                    # whole 16-byte exchange units (pairs of rows)
             mine = self._buf("d_pairs_loc", (Bp, 2), torch.float32)
@@ -776,6 +795,11 @@ class PaliGemmaEngine:
         kvd = nkv * hd
         so, sd = self.split_o, self.split_down
         attn = self._buf("d_attn", (B, nh * hd), torch.bfloat16)
+        # 17..32 rows on the fp8 GEMV, one rank: o_proj / down_proj may add their partials into the residual with
+        # float atomics (no slabs for the next norm to re-read), as the batch-1 path does.  Measured slower at pt-896
+        # x32 (down 11.5 -> 14.9 us: the MFMA output layout scatters each atomic instruction over 16 rows), so off
+        add = (self.tp == 1 and self.DECODE_ADD_B32 and self.FP8_GEMV and self._fp8_rows(B) and B <= 32
+               and "o_w8f" in w.tl[0] and "down_w8f" in w.tl[0])
         ns = 0
         for i, Lw in enumerate(w.tl):
             xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
@@ -785,12 +809,20 @@ class PaliGemmaEngine:
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             a8 = self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS,
                                           nsplit, want_fp8=self._fp8_rows(B))
-            self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
-            n_o = self._allreduce_slabs(part, so)
+            if add:
+                self._lin(a8 or attn, Lw, "o", res, ops.EPI_F32_ADD, B, ksplit=so)
+                n_o = 0
+            else:
+                self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
+                n_o = self._allreduce_slabs(part, so)
             xin = self._norm(res, Lw["post_w"], part, n_o, xn, B)
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
-            self._lin(h, Lw, "down", part, ops.EPI_F32, B, ksplit=sd)
-            ns = self._allreduce_slabs(part, sd)
+            if add:
+                self._lin(h, Lw, "down", res, ops.EPI_F32_ADD, B, ksplit=sd)
+                ns = 0
+            else:
+                self._lin(h, Lw, "down", part, ops.EPI_F32, B, ksplit=sd)
+                ns = self._allreduce_slabs(part, sd)
         return ns
 
     def sample(self, logits: torch.Tensor, st: dict, sampler: dict, advance: bool,

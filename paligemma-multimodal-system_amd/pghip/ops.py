@@ -108,9 +108,10 @@ def quant_fp8(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional
 
 def gemm8(A8: torch.Tensor, a_scale: torch.Tensor, W8: torch.Tensor, w_scale: torch.Tensor, out: torch.Tensor, *,
           epi: int = EPI_BF16, M: Optional[int] = None, bias: Optional[torch.Tensor] = None, ksplit: int = 1,
-          fa=None) -> torch.Tensor:
+          fa=None, frag: bool = False) -> torch.Tensor:
     """fp8 GEMM: out = epilogue((A8 . W8^T) * a_scale[m] * w_scale[n]) (PG_FP8, pg_gemm_fused).  A8, W8 are
-    uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE."""
+    uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE.
+    frag: W8 is fp8 fragment-packed (weights.frag_pack8) -> the weight-streaming fp8 GEMV, M <= 32."""
     for t, n in ((A8, "A8"), (W8, "W8")):
         if t.dtype != torch.uint8 or not t.is_cuda or t.stride(1) != 1:
             raise ValueError(f"pghip.gemm8: {n} must be a row-major uint8 (e4m3) HIP tensor")
@@ -122,6 +123,12 @@ def gemm8(A8: torch.Tensor, a_scale: torch.Tensor, W8: torch.Tensor, w_scale: to
     fa.a_scale, fa.w_scale = a_scale.data_ptr(), w_scale.data_ptr()
     e = epi & 0xFF
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
+    if frag:
+        if M > 32:
+            raise ValueError("pghip.gemm8: the fp8 GEMV takes at most 32 rows")
+        _lib.call("pg_gemm_fused", _p(A8), A8.stride(0), _p(W8), W8.stride(0), _p(bias), _p(out), ldc, M, N, K,
+                  e | EPI_FP8 | W_FRAG, ksplit, _lib.C.byref(fa), _s())
+        return out
     s = finalize_split(M, N, K // 2) if ksplit == 1 and e in _FIN_EPIS else 1
     if s > 1:   # small M: fp32 slabs, then the epilogue (scales already applied inside the slabs)
         part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)

@@ -53,6 +53,23 @@ def frag_unpack(p: torch.Tensor) -> torch.Tensor:
     return p.reshape(N // 16, K // 64, 2, 4, 16, 8).permute(0, 4, 1, 3, 2, 5).contiguous().view(N, K)
 
 
+def frag_pack8(w8: torch.Tensor) -> torch.Tensor:
+    """Row-major e4m3 bytes W8[N][K] (uint8, N % 16 == 0, K % 128 == 0) -> the fp8 fragment-packed layout of
+    include/pghip.h (PG_FP8 | PG_W_FRAG, the fp8 decode GEMV): W8[16t + r][128c + 64s + 16g + e] at byte
+    ((t*K/128 + c)*2 + s)*1024 + (16g + r)*16 + e, so each (16-row x 128-k chunk, piece s) is one 1-KiB lane-linear
+    wave load.  Same shape [N][K]."""
+    N, K = w8.shape
+    if N % 16 or K % 128 or w8.dtype != torch.uint8:
+        raise ValueError(f"frag_pack8 needs uint8 [N][K] with N % 16 == 0 and K % 128 == 0, got {tuple(w8.shape)}")
+    return w8.reshape(N // 16, 16, K // 128, 2, 4, 16).permute(0, 2, 3, 4, 1, 5).contiguous().view(N, K)
+
+
+def frag_unpack8(p: torch.Tensor) -> torch.Tensor:
+    """Inverse of frag_pack8."""
+    N, K = p.shape
+    return p.reshape(N // 16, K // 128, 2, 4, 16, 16).permute(0, 4, 1, 2, 3, 5).contiguous().view(N, K)
+
+
 def rope_row_perm(D: int) -> torch.Tensor:
     """Row order inside one D-wide head block for the fused RoPE epilogue: 16-row tile t holds
     dims 8t..8t+7 then D/2+8t..D/2+8t+7, so each lane's rotate_half partner is lane ^ 32."""
@@ -238,9 +255,19 @@ class PackedWeights:
                     raise ValueError("fp8 weights need hidden and heads*head_dim multiples of 128")
                 for name, m in (("qkv", qkv_w), ("o", o_w), ("gu", gu), ("down", down)):
                     layer[name + "_w8"], layer[name + "_s8"] = quant_rows_fp8(m)
+                    if m.shape[0] % 16 == 0 and m.shape[1] % 128 == 0:
+                        # fragment-packed copy for the fp8 decode GEMV (17..32 rows; the tile GEMMs read _w8)
+                        layer[name + "_w8f"] = frag_pack8(layer[name + "_w8"])
             self.tl.append(layer)
             del qkv_w, o_w, gu, down
             del g, u
+        self.lm_w8f = self.lm_s8 = None
+        if self.fp8 and self.hidden % 128 == 0 and self.vocab_local_pad % 16 == 0:
+            # the tied lm_head as fp8 rows too (per-row scales, fragment-packed) for the batch > 16 decode GEMV
+            lmr = frag_unpack(self.lm_w) if self.frag else self.lm_w
+            w8, self.lm_s8 = quant_rows_fp8(lmr)
+            self.lm_w8f = frag_pack8(w8)
+            del lmr, w8
         self.final_w = f32(get(lm + "model.norm.weight"))
         self.wflag = 0x100 if self.frag else 0            # ops.W_FRAG for every Gemma linear
         self.qkv_n = (self.heads + 2 * self.kv_heads) * hd
@@ -261,7 +288,10 @@ class PackedWeights:
         return n + self.lm_w.numel() * 2
 
     def decode_weight_bytes_fp8(self) -> int:
-        """The same for the fp8 path (batch > 16 decode): e4m3 linears + scales, bf16 lm_head."""
+        """The same for the fp8 path (batch > 16 decode): e4m3 linears + scales, e4m3 lm_head + scales (bf16 when
+        no fp8 copy was packed)."""
         n = sum(sum(d[k + "_w8"].numel() + d[k + "_s8"].numel() * 4 for k in ("qkv", "o", "gu", "down"))
                 for d in self.tl)
+        if self.lm_w8f is not None:
+            return n + self.lm_w8f.numel() + self.lm_s8.numel() * 4
         return n + self.lm_w.numel() * 2

@@ -883,3 +883,36 @@ def test_norm_residual_fp8_equals_quantised_bf16_output(M, H, nsplit):
     assert torch.equal(r1, r2)
     assert torch.equal(s, s_ref)
     assert torch.equal(q, q_ref)
+
+
+@pytest.mark.parametrize("M,N,K,ks", [(32, 2560, 2048, 1), (17, 2048, 16384, 8), (24, 4096, 2048, 2),
+                                      (9, 512, 256, 1), (32, 32160, 2048, 1), (32, 16384, 2048, 1)])
+def test_gemv8_fragment_packed_matches_the_fp8_tile_gemm(M, N, K, ks):
+    """The fp8 weight-streaming GEMV (fragment-packed e4m3 weights, weights.frag_pack8; 17..32-row batched decode and
+    the fp8 lm_head): equal to a torch fp32 matmul of the dequantised operands up to fp32 summation order, for the
+    fp32 slab (split-K), bf16 and gelu*up epilogues; the pack / unpack pair is a bijection."""
+    from pghip import ops
+    from pghip.weights import frag_pack8, frag_unpack8, quant_rows_fp8
+    A, W = rnd(M, K, seed=71), rnd(N, K, scale=1 / math.sqrt(K), seed=72)
+    bias = torch.randn(N).cuda()
+    a8, sa = ops.quant_fp8(A)
+    w8, sw = quant_rows_fp8(W)
+    w8f = frag_pack8(w8)
+    assert torch.equal(frag_unpack8(w8f), w8)
+    ref = _deq(a8, sa) @ _deq(w8, sw).t()
+    part = torch.empty(ks, M, N, dtype=torch.float32, device="cuda")
+    ops.gemm8(a8, sa, w8f, sw, part, epi=ops.EPI_F32, bias=bias, ksplit=ks, frag=True)
+    assert err(part.sum(0), ref + bias) < 5e-5
+    resid = torch.randn(M, N).cuda()                  # the float-atomic residual add (batched fp8 decode)
+    r0 = resid.clone()
+    ops.gemm8(a8, sa, w8f, sw, resid, epi=ops.EPI_F32_ADD, bias=bias, ksplit=ks, frag=True)
+    assert err(resid - r0, ref + bias) < 5e-5
+    if ks == 1:
+        outb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        ops.gemm8(a8, sa, w8f, sw, outb, epi=ops.EPI_BF16, bias=bias, frag=True)
+        assert err(outb, ref + bias) < 1e-2
+        h = torch.empty(M, N // 2, dtype=torch.bfloat16, device="cuda")
+        ops.gemm8(a8, sa, w8f, sw, h, epi=ops.EPI_BF16_GELU_MUL, frag=True)
+        g = ref.view(M, N // 32, 2, 16)
+        want = (torch.nn.functional.gelu(g[:, :, 0], approximate="tanh") * g[:, :, 1]).reshape(M, N // 2)
+        assert err(h, want) < 1e-2

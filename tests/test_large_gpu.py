@@ -6,8 +6,11 @@ Tolerances, as test_engine_gpu.py's full-size pt-224 tests (the synthetic 2/sqrt
 rounding to ~10% of the logit scale end to end, so the end-to-end bound is relative to that, and the kernels are
 checked layer by layer without accumulation):
   * every SigLIP / Gemma layer, fed the HIP path's own input, matches the fp32 oracle layer to < 2e-2 (scaled);
-  * the reference's top-64 logits of every teacher-forced step lie within 15% of their scale (bf16), 30% (fp8
-    e4m3 Gemma linears, 3 mantissa bits: the per-row / per-channel scaled operands add their own rounding);
+  * the reference's top-64 logits of every teacher-forced step lie within 15% of their scale (bf16); with fp8
+    e4m3 operands within 1.5x the distance of the fp32 oracle run on the same operand rounding (a fixture of
+    tests/golden/make_emu.py: derived per image and step, not a flat percentage);
+  * free-running greedy ids equal the reference's exactly at pt-448 x 16 (two images) and pt-896 (bf16), on the
+    better-conditioned synthetic recipe whose margins exceed the bf16 error (tests/golden/pt448wc.npz, pt896wc.npz);
   * the top-1 id equals the reference's wherever the reference's top1-top2 margin exceeds twice that step's
     measured error;
   * the rows of a batch that hold the same request agree to 2e-2 (scaled): rows in a ragged last row block run
@@ -40,10 +43,10 @@ def _pixels(g, j, size):
     return pv
 
 
-def _engine(name, fp8=False):
+def _engine(name, fp8=False, linear_gain=2.0):
     from pghip import configs, engine, synthetic, weights
     cfg = configs.CONFIGS[name]
-    sd = synthetic.SyntheticStateDict(cfg)
+    sd = synthetic.SyntheticStateDict(cfg, linear_gain=linear_gain)
     return cfg, sd, engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=fp8))
 
 
@@ -151,27 +154,86 @@ def test_pt896_layers_vs_oracle_and_reference(golden):
     _check_step(lg, g, "i0_", 0, 0.15, [])
 
 
-def test_pt896_batch32_fp8_vs_reference(golden):
-    """BASELINE configs[4] on one device: pt-896 at batch 32 with the Gemma linears on the fp8 e4m3 MFMA (per-row /
-    per-channel scales), prefill (131 k rows) and teacher-forced decode steps over 4.1 k keys (multi-block split-KV
-    decode attention, fp8 GEMMs of 32 rows): every 8th row against the reference (30% bound), all rows of the
-    batch equal to each other."""
-    g = golden("pt896")
-    cfg, sd, eng = _engine("pt-896", fp8=True)
-    pv = _pixels(g, 0, 896)
+def _fp8_batch32(golden, name, images):
+    """BASELINE configs[4] on one device: pt-896 at batch 32 with the Gemma linears and (at 17..32 rows) the lm_head
+    on e4m3 operands (per-row / per-channel scales): the fp8 tile GEMMs of the 131 k-row prefill and the fp8 GEMVs of
+    the teacher-forced decode steps over 4.1 k keys.  32 rows dealt in equal blocks to the golden's images.  Bound,
+    per image and step: the reference's top-64 logits within 1.5x the distance of the fp32 oracle run on the same
+    e4m3 / bf16 operand rounding (tests/golden/make_emu.py, <name>_fp8emu.npz) -- derived, not a flat percentage; the
+    top-1 id equal to the reference's wherever its margin exceeds twice the step's measured error (a minimum count of
+    such checks is asserted); rows of one image equal to each other (< 2e-2)."""
+    g, em = golden(name), golden(name + "_fp8emu")
+    gain = float(g["linear_gain"]) if "linear_gain" in g else 2.0
+    cfg, sd, eng = _engine("pt-896", fp8=True, linear_gain=gain)
     B = 32
-    ids = torch.from_numpy(np.concatenate([g["i0_input_ids"]] * B)).cuda()
-    px = torch.from_numpy(np.concatenate([pv] * B)).cuda()
-    steps = len(g["i0_greedy_ids"])
+    per = B // len(images)
+    pvs = [_pixels(g, j, 896) for j in images]
+    ids = torch.from_numpy(np.concatenate([g[f"i{j}_input_ids"] for j in images for _ in range(per)])).cuda()
+    px = torch.from_numpy(np.concatenate([pv for pv in pvs for _ in range(per)])).cuda()
+    steps = len(g[f"i{images[0]}_greedy_ids"])
     cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), steps + 2)
     st = eng.decode_state(B, cache, nxt, steps + 2)
-    worst = 0.0
+    checked, worst = [], 0.0
     for t in range(steps):
         if t > 0:
-            st["ids"].fill_(int(g["i0_greedy_ids"][t - 1]))
+            for k, j in enumerate(images):
+                st["ids"][k * per:(k + 1) * per].fill_(int(g[f"i{j}_greedy_ids"][t - 1]))
             logits = eng.decode_step(st, cache, feats, dict(do_sample=False))
         lg = logits.cpu().numpy()
-        for r in range(0, B, 8):
-            worst = max(worst, _check_step(lg[r], g, "i0_", t, 0.30, []))
-        assert err(lg, np.broadcast_to(lg[0], lg.shape)) < 2e-2, t
-    print(f"pt896 x32 fp8: worst top-64 error {worst:.4f}")
+        for k, j in enumerate(images):
+            p = f"i{j}_"
+            rows = lg[k * per:(k + 1) * per]
+            top_v = g[p + "step_top_values"][t]
+            emu = float(np.abs(em[p + "emu_top_values"][t] - top_v).max())
+            tol = 1.5 * emu / float(np.abs(top_v).max())
+            for r in (0, per - 1):
+                worst = max(worst, _check_step(rows[r], g, p, t, tol, checked) / emu)
+            assert err(rows, np.broadcast_to(rows[0], rows.shape)) < 2e-2, (j, t)
+    print(f"{name} x32 fp8: worst top-64 error {worst:.3f}x the emulated e4m3 distance, top-1 checked at "
+          f"{len(checked)} (row, step) pairs")
+    return checked
+
+
+def test_pt896_batch32_fp8_vs_reference(golden):
+    """The default recipe's pt-896 request (tests/golden/pt896.npz, 3 steps) on all 32 rows.  Its top1-top2 margins
+    (0.03-0.20) lie below the e4m3 operands' error (the emulation itself flips step 1's argmax), so the top-1 ids are
+    checked on the better-conditioned recipe below; here the bound on the top-64 logits carries the check."""
+    _fp8_batch32(golden, "pt896", [0])
+
+
+def test_pt896_batch32_fp8_two_images_vs_reference(golden):
+    """The better-conditioned recipe's two pt-896 requests (tests/golden/pt896wc.npz, 16 steps), 16 rows each."""
+    checked = _fp8_batch32(golden, "pt896wc", [0, 1])
+    assert len(checked) >= 40, checked          # 2 images x 2 rows x 16 steps; step 0's small margins may skip
+
+
+def test_pt448_batch16_free_running_greedy_ids_equal_reference(golden):
+    """BASELINE configs[2] (pt-448, batch 16) free-running: two images (tests/golden/pt448wc.npz seeds 1236 / 1237,
+    the two whose first-token margins exceed 0.1 on the better-conditioned recipe), 8 rows each, 24 greedy tokens
+    through the bench's decode path (chained argmax + embed, hipGraph replay): every row's ids equal the reference's
+    own loop exactly -- one differing id fails."""
+    g = golden("pt448wc")
+    cfg, sd, eng = _engine("pt-448", linear_gain=float(g["linear_gain"]))
+    images = [2, 3]
+    pvs = [_pixels(g, j, 448) for j in images]
+    ids = torch.from_numpy(np.concatenate([g[f"i{j}_input_ids"] for j in images for _ in range(8)])).cuda()
+    px = torch.from_numpy(np.concatenate([pv for pv in pvs for _ in range(8)])).cuda()
+    steps = len(g["i2_greedy_ids"])
+    out = eng.generate(ids, px, torch.ones_like(ids), steps, stop_token=None)
+    for k, j in enumerate(images):
+        want = g[f"i{j}_greedy_ids"].tolist()
+        for r in range(8):
+            assert out[k * 8 + r].tolist() == want, (j, r, out[k * 8 + r].tolist(), want)
+
+
+def test_pt896_free_running_greedy_ids_equal_reference(golden):
+    """pt-896 (4096 image tokens, bf16) free-running: the two requests of tests/golden/pt896wc.npz as one batch of 2,
+    16 greedy tokens each through the bench's decode path: ids equal to the reference's loop exactly."""
+    g = golden("pt896wc")
+    cfg, sd, eng = _engine("pt-896", linear_gain=float(g["linear_gain"]))
+    pvs = [_pixels(g, j, 896) for j in (0, 1)]
+    ids = torch.from_numpy(np.concatenate([g["i0_input_ids"], g["i1_input_ids"]])).cuda()
+    px = torch.from_numpy(np.concatenate(pvs)).cuda()
+    out = eng.generate(ids, px, torch.ones_like(ids), len(g["i0_greedy_ids"]), stop_token=None)
+    for j in (0, 1):
+        assert out[j].tolist() == g[f"i{j}_greedy_ids"].tolist(), (j, out[j].tolist())
