@@ -119,7 +119,7 @@ def time_dominant_kernel(eng, reps=50):
 
 def pmc_traffic():
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 --pmc passes
-    (scripts/gpu_pmc.sh -> profiles/*pmc_gateup.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE), or None."""
+    (scripts/gpu_pmc_gateup.sh -> profiles/*pmc_gateup.json: FETCH_SIZE x2 (gfx950) + WRITE_SIZE), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_gateup.json")))
     if not files:
