@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -90,6 +90,15 @@ typedef struct PgFusedArgs {
   void* kd;                 /* PG_EPI_QKV_ROPE (ABI 6, may be null): decode-order copies of the cache, [B][Hkv][Smax][D]
                                each, written beside kc / vtc (element offsets: csrc/attn_common.h dec_koff / dec_voff) */
   void* vd;
+  /* ABI 9 -- the batched fp8 decode MLP without a quantiser launch (BASELINE configs[4]):                         */
+  unsigned* amax_out;       /* PG_EPI_BF16_GELU_MUL with PG_FP8|PG_W_FRAG (optional): max |bf16 output| of row m is
+                               atomically max-ed into amax_out[m * amax_ld] (float bits; zero beforehand)          */
+  const unsigned* amax_in;  /* pro_mode 5 (PG_FP8|PG_W_FRAG, PG_EPI_F32, M <= 32): A is bf16 [M][lda elements],
+                               quantised to e4m3 while staged, row scale s[m] = amax_in[m * amax_ld] / 448 (1 when
+                               zero) -- pg_quant_fp8's bytes and scale; a_scale is not read                          */
+  int amax_ld;
+  unsigned* amax_zero;      /* optional, any PG_FP8|PG_W_FRAG launch: amax_zero[0 .. amax_zero_n) set to 0 (n <= 4096) */
+  int amax_zero_n;
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -151,12 +160,15 @@ int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, in
 
 /* Batched split-KV decode attention with the split merge in the same launch (gemma.py:307-339 for one new position
  * per row; replaces pg_attention(split) + pg_attn_combine for B > 2, ABI 5).  The kcap/32 cache blocks of a
- * (batch, kv head) are dealt round-robin to nsplit splits of nw (2 or 4) waves, nb rounds each (nw*nsplit <=
+ * (batch, kv head) are cut into nsplit contiguous ranges for splits of nw (2 or 4) waves, nb rounds each (nw*nsplit <=
  * kcap/32 <= nw*nsplit*nb); the last-arriving split (one agent-scope ticket in counters[b*Hkv + kvh], left zero)
  * merges the partials and writes o[b][hq][0..D) bf16.  D = 32 or 256.  The cache must hold finite values in every
  * row below kcap (masked keys get weight 0 but their V is not zeroed).  q8 (optional, ABI 7; Hkv == 1 and
  * Hq*D/8 <= nw*64): the merging workgroup also writes the row as fp8 e4m3, q8[b*q8_ld + hq*D + d], with
- * q8_scale[b] -- the bytes pg_quant_fp8 makes from o, so the fp8 o_proj needs no quantiser launch. */
+ * q8_scale[b] -- the bytes pg_quant_fp8 makes from o, so the fp8 o_proj needs no quantiser launch.
+ * nw | PG_ATTN_PIPE (D == 256, nw == 4, nb >= 2; ignored otherwise): the double-buffered form, one round's K/V in
+ * flight while the previous round is computed (one wave per SIMD: for grids of at most one workgroup per CU). */
+#define PG_ATTN_PIPE 0x100
 int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, const void* kd, const void* vd, int B, int Lkv,
                    const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit, int nw, int nb,
                    float* part_o, float* part_ml, int* counters, void* q8, float* q8_scale, long q8_ld,

@@ -29,6 +29,7 @@
 #define PG_COMBINE_PF 12  // split-KV merge: O partials of the first 12 splits per thread loaded up front
 #endif
 #ifndef PG_ATTN_WG
+#define PG_ATTN_PIPE 0x100 // pg_attn_decode: flag OR-ed into nw -- the double-buffered form (include/pghip.h)
 #define PG_ATTN_WG 1      // decode splits of 2 / 4 / 8 blocks (head_dim 256): one wave per block, merged in LDS
 #endif
 #ifndef PG_ATTN_SPLIT_WAVES
@@ -124,18 +125,20 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
 }
 
 // Batched decode (B > 2: the batch alone fills the chip) with the split merge in the same launch.
-// One workgroup of NW waves per (split, kv head, batch).  The cache is dealt to the S splits in granules of NW
-// consecutive 32-key blocks, round-robin (granule i -> split i % S; round j of a split takes its j-th granule, wave
-// w its w-th block), so every split gets the same number of blocks whatever the cache length and the two 64-B
-// halves of a 128-B V^T line (adjacent blocks) are read by one CU (dealing single blocks round-robin put them on
-// two XCDs, each fetching the whole line).  The NW running (O, m, l)
+// One workgroup of NW waves per (split, kv head, batch).  Split sp owns the contiguous 32-key blocks
+// [sp * nblk / S, (sp + 1) * nblk / S) -- floor or ceil of nblk / S each -- and its wave w takes every NW-th of them
+// from the w-th, so the two 64-B halves of a 128-B V^T line (adjacent blocks) are read by one CU (dealing single
+// blocks round-robin put them on two XCDs, each fetching the whole line).  The NW running (O, m, l)
 // merge through LDS into the split's partial, stored write-through (sc1); one agent-scope ticket per (batch,
 // kv head) then makes the workgroup of the last-arriving split merge the S partials (sc1 loads: the MI355X guide's
 // in-launch hand-off with no release / acquire fence) and write the bf16 attention rows -- no combine launch.
 // Stamps of the one-wave-per-split kernel it replaces for B > 2 (scripts/tune/attn_stamps.py): at 340 registers
 // (one wave per SIMD) a split's compute (0.9 us) never overlapped another split's loads, and pt-896 x32 ran 4.25
 // rounds of waves (54 us for 142 MB of K/V); this kernel holds 240 registers (two waves per SIMD).
-template <int DP, int DT, int NW>
+// PIPE: each wave's blocks are staggered -- the next block's K / V loads are issued between the current block's
+// phases, so its loads never drain during a compute phase (one wave per SIMD at pt-896 x32: each round's compute,
+// 0.9 us, stalled the stream of the single-buffered form).
+template <int DP, int DT, int NW, bool PIPE>
 __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs a, int nb, int* __restrict__ cnt,
                                                                       uint8_t* __restrict__ q8, float* __restrict__ q8s,
                                                                       long q8_ld) {
@@ -145,6 +148,9 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   const int S = gridDim.x, sp = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int G = a.G;
   const int rr = c < G ? c : G - 1;                // rows past G read row G - 1 (never stored): no select
+#if PG_ATTN_STAMPS
+  unsigned long long st0 = __builtin_amdgcn_s_memrealtime(), st1 = 0, st2 = 0, st3 = 0;
+#endif
   const int lkv_raw =
       __hip_atomic_load(a.lkv_dev ? a.lkv_dev : &pg_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the G query rows of this (batch, kv head) in LDS, re-read per block (32 registers fewer: two waves per SIMD)
@@ -161,7 +167,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   __builtin_amdgcn_sched_barrier(0);               // (the q loads stay ahead of the K/V stream)
   const bf16_t* kbase = a.kd + ((long)b * a.Hkv + kvh) * a.kcap * DP;   // decode-order copies
   const bf16_t* vbase = a.vd + ((long)b * a.Hkv + kvh) * a.kcap * DP;
+  // split sp owns the contiguous blocks [lo, hi) (at least NW: nsplit <= kcap / 128), wave w the blocks lo + w +
+  // NW * j: every split reads ceil or floor of nblk / S blocks (dealing granules of NW blocks round-robin left the
+  // first splits a whole extra round: pt-896 x32, 131 blocks, 20 vs 17 per CU)
   const int nblk = a.kcap >> 5;
+  const int lo = (int)((long)sp * nblk / S), hi = (int)((long)(sp + 1) * nblk / S);
   auto qfrag = [&](bf16x8 (&qf)[KS]) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) qf[s] = __builtin_bit_cast(bf16x8, sq[rr][4 * s + g]);
@@ -173,8 +183,8 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
   // round 0 (every split owns at least NW blocks: nsplit <= kcap / 128): its loads are issued before the kv length
-  // arrives; later rounds skip blocks past the cache (wave-uniform)
-  int blk = sp * NW + wave;
+  // arrives
+  int blk = lo + wave;
   dec_load_block<DP, DT>(a, kbase, vbase, 32 * blk, c, g, kfa, kfb, vr);
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -185,22 +195,70 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   __syncthreads();                                 // sq written (the block's loads stay in flight across it)
   __builtin_amdgcn_sched_barrier(0);
   const int Lkv = __builtin_amdgcn_readfirstlane(lkv_raw) + a.Lkv;
-  {
+  if constexpr (!PIPE) {
+    {
+      bf16x8 qf[KS];
+      qfrag(qf);
+      dec_block_update<DP, DT, false, true>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr,
+                                            o, m, l);
+    }
+    for (int j = 1; j < nb; ++j) {
+      blk = lo + NW * j + wave;
+      if (blk >= hi) break;
+      dec_load_block<DP, DT>(a, kbase, vbase, 32 * blk, c, g, kfa, kfb, vr);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 qf[KS];
+      qfrag(qf);
+      dec_block_update<DP, DT, false>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr, o,
+                                      m, l);
+    }
+  } else {
+    // staggered: block j + 1's K is issued as soon as block j's scores are out of the K registers, its V as soon as
+    // block j's P.V is out of the V registers -- one block of loads stays in flight through every compute phase with
+    // no second register set.  The loads are unconditional inside the loop (wave-uniform trip count n - 1), so both
+    // edges into the loop head carry the same [K, V] loads in flight and the compiler's vmcnt waits for the older half.
+    const int n = (hi - lo - wave + NW - 1) / NW;  // this wave's blocks (>= 1)
+    auto ldk = [&](int bk) {
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) {
+        const int kl = min(32 * bk, a.kcap - 32);
+        kfa[s2] = *(const u32x4*)(kbase + dec_kfrag(kl, 0, s2, c, g, DP));
+        kfb[s2] = *(const u32x4*)(kbase + dec_kfrag(kl, 1, s2, c, g, DP));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto ldv = [&](int bk) {
+      const int kl = min(32 * bk, a.kcap - 32);
+#pragma unroll
+      for (int t = 0; t < DT; ++t) vr[t] = *(const u32x4*)(vbase + dec_vfrag(kl, t, c, g, DP));
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto none = [] {};
     bf16x8 qf[KS];
     qfrag(qf);
-    dec_block_update<DP, DT, false, true>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr,
-                                          o, m, l);
+    if (n > 1) {
+      dec_block_update<DP, DT, false, true>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr,
+                                            o, m, l, [&] { ldk(blk + NW); });
+      ldv(blk + NW);
+      for (int j = 1; j < n - 1; ++j) {
+        blk += NW;
+        qfrag(qf);
+        dec_block_update<DP, DT, false>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr, o,
+                                        m, l, [&] { ldk(blk + NW); });
+        ldv(blk + NW);
+      }
+      blk += NW;
+      qfrag(qf);
+      dec_block_update<DP, DT, false>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr, o, m,
+                                      l, none);
+    } else {
+      dec_block_update<DP, DT, false, true>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr,
+                                            o, m, l, none);
+    }
   }
-  for (int j = 1; j < nb; ++j) {
-    blk = (sp + S * j) * NW + wave;
-    if (blk >= nblk) break;
-    dec_load_block<DP, DT>(a, kbase, vbase, 32 * blk, c, g, kfa, kfb, vr);
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8 qf[KS];
-    qfrag(qf);
-    dec_block_update<DP, DT, false>(a.scale_log2, 32 * blk, min(Lkv, 32 * blk + 32), c, g, qf, kfa, kfb, vr, o, m,
-                                    l);
-  }
+#if PG_ATTN_STAMPS
+  PG_STAMP(st1);
+#endif
   // the NW waves' (O, m, l) -> the split's partial (wave 0), 2^(m_w - M) weights
   __shared__ f32x4 so[NW > 1 ? NW - 1 : 1][DT][64];
   __shared__ float sml[NW > 1 ? NW - 1 : 1][2][16];
@@ -246,6 +304,15 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   if (threadIdx.x == 0)
     s_last = __hip_atomic_fetch_add(cnt + b * a.Hkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
   __syncthreads();
+#if PG_ATTN_STAMPS
+  PG_STAMP(st2);
+  st3 = st2;
+  const int sid = (b * a.Hkv + kvh) * S + sp;
+  if (threadIdx.x == 0 && sid < 8192 && !s_last) {
+    pg_attn_stamp_buf[sid][0] = st0; pg_attn_stamp_buf[sid][1] = st1;
+    pg_attn_stamp_buf[sid][2] = st2; pg_attn_stamp_buf[sid][3] = 0;
+  }
+#endif
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        // compiler-only: the loads stay below the ticket
   // the last split's workgroup merges the S partials: one thread per (q row, 8 dims), 16 splits per round trip
@@ -315,6 +382,13 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
     }
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt + b * a.Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if PG_ATTN_STAMPS
+  PG_STAMP(st3);
+  if (threadIdx.x == 0 && sid < 8192) {
+    pg_attn_stamp_buf[sid][0] = st0; pg_attn_stamp_buf[sid][1] = st1;
+    pg_attn_stamp_buf[sid][2] = st2; pg_attn_stamp_buf[sid][3] = st3;
+  }
+#endif
 }
 
 template <int DP, int DT>
@@ -1172,6 +1246,8 @@ extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, cons
                               int nw, int nb, float* part_o, float* part_ml, int* counters, void* q8,
                               float* q8_scale, long q8_ld, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && (D == 32 || D == 256));
+  const bool pipe = (nw & PG_ATTN_PIPE) != 0 && nb >= 2;      // the double-buffered form (head_dim 256, 4 waves)
+  nw &= ~PG_ATTN_PIPE;
   // the fp8 copy: the merging workgroup holds the whole row (one kv head, one item per thread)
   if (q8) PG_REQUIRE(Hkv == 1 && Hq * (D / 8) <= nw * 64 && q8_scale && q8_ld >= (long)Hq * D && q8_ld % 8 == 0 &&
                      ((uintptr_t)q8 & 7) == 0);
@@ -1184,18 +1260,20 @@ extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, cons
              1, Lkv, Hq / Hkv, Hkv, D, lkv_dev, scale * 1.4426950408889634f, 32 * 4 * nb, part_o, part_ml, kcap, 0,
              (const bf16_t*)kd, (const bf16_t*)vd};
   const dim3 grid(nsplit, Hkv, B);
-  if (D == 256 && nw == 4)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 4>), grid, dim3(256), 0, stream, a, nb, counters,
-                       (uint8_t*)q8, q8_scale, q8_ld);
+#define PG_DEC_LAUNCH(DP_, DT_, NW_, PIPE_)                                                                 \
+  hipLaunchKernelGGL((attn_decode_fused_kernel<DP_, DT_, NW_, PIPE_>), grid, dim3(NW_ * 64), 0, stream, a, nb, \
+                     counters, (uint8_t*)q8, q8_scale, q8_ld)
+  if (D == 256 && nw == 4 && pipe)
+    PG_DEC_LAUNCH(256, 16, 4, true);
+  else if (D == 256 && nw == 4)
+    PG_DEC_LAUNCH(256, 16, 4, false);
   else if (D == 256)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<256, 16, 2>), grid, dim3(128), 0, stream, a, nb, counters,
-                       (uint8_t*)q8, q8_scale, q8_ld);
+    PG_DEC_LAUNCH(256, 16, 2, false);
   else if (nw == 4)
-    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 4>), grid, dim3(256), 0, stream, a, nb, counters,
-                       (uint8_t*)q8, q8_scale, q8_ld);
+    PG_DEC_LAUNCH(32, 2, 4, false);
   else
-    hipLaunchKernelGGL((attn_decode_fused_kernel<32, 2, 2>), grid, dim3(128), 0, stream, a, nb, counters,
-                       (uint8_t*)q8, q8_scale, q8_ld);
+    PG_DEC_LAUNCH(32, 2, 2, false);
+#undef PG_DEC_LAUNCH
   PG_LAUNCH_CHECK();
   return 0;
 }

@@ -414,11 +414,15 @@ __device__ __forceinline__ void dec_load_block(const AttnArgs& a, const bf16_t* 
 // accumulators, the key order inside the k-step permuted identically for V^T (lane holds keys 4g.., 16 + 4g..).
 // MASK_V = false: V^T past kend is not zeroed (P is 0 there already): only for caches that hold finite values in every
 // row (the engine's zero-initialised static cache, written only with model outputs) -- saves 64 registers.
-template <int DP, int DT, bool MASK_V = true, bool FIRST = false>
+// mid() runs once the scores are computed (the K registers are free: the staggered caller issues the next K there).
+struct DecNoMid {
+  __device__ void operator()() const {}
+};
+template <int DP, int DT, bool MASK_V = true, bool FIRST = false, typename Mid = DecNoMid>
 __device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int kend, int c, int g,
                                                  const bf16x8 (&qf)[DP / 32], const u32x4 (&kfa)[DP / 32],
                                                  const u32x4 (&kfb)[DP / 32], const u32x4 (&vr)[DT],
-                                                 f32x4 (&o)[DT], float& m, float& l) {
+                                                 f32x4 (&o)[DT], float& m, float& l, Mid mid = Mid()) {
   (void)c;
   u32x4 vf[DT];
 #pragma unroll
@@ -434,6 +438,7 @@ __device__ __forceinline__ void dec_block_update(float scale_log2, int kb, int k
     sA = mfma16(__builtin_bit_cast(bf16x8, kfa[s]), qf[s], sA);
     sB = mfma16(__builtin_bit_cast(bf16x8, kfb[s]), qf[s], sB);
   }
+  mid();
   float x[8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

@@ -91,6 +91,14 @@ struct PgFusedArgs {
   // dec_voff), [B][Hkv][Smax][D] each: every appended k / v is also written there
   bf16_t* kd;
   bf16_t* vd;
+  // ABI 9: the batched fp8 decode MLP without a quantiser launch -- the gate/up epilogue max-es each row's |h| into
+  // amax_out (float bits); pro_mode 5 (down) stages bf16 h quantised with amax_in / 448; amax_zero is cleared by
+  // the first workgroup of any fp8 GEMV launch (the QKV GEMV of the same layer)
+  unsigned* amax_out;
+  const unsigned* amax_in;
+  int amax_ld;
+  unsigned* amax_zero;
+  int amax_zero_n;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -282,6 +290,25 @@ __device__ __forceinline__ void epi_gelu_mul4(const EpiArgs& e, int m, int gb, i
   *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + oc) = p;
 }
 
+// epi_gelu_mul4 that also returns max |bf16 output| of the four (0 when not stored): the per-row amax the fp8 down
+// projection's prologue quantises h with (PgFusedArgs.amax_out / amax_in, pg_quant_fp8's rule)
+__device__ __forceinline__ float epi_gelu_mul4_amax(const EpiArgs& e, int m, int gb, int q, f32x4 g, f32x4 u) {
+  if (m >= e.M) return 0.f;
+  const int oc = (gb >> 1) + q;
+  if (oc + 3 >= (e.N >> 1)) return 0.f;
+  u32x2 p;
+  p[0] = pack_bf2(gelu_tanh(g[0]) * u[0], gelu_tanh(g[1]) * u[1]);
+  p[1] = pack_bf2(gelu_tanh(g[2]) * u[2], gelu_tanh(g[3]) * u[3]);
+  *(u32x2*)((bf16_t*)e.C + (size_t)m * e.ldc + oc) = p;
+  return fmaxf(fmaxf(fabsf(bf_lo(p[0])), fabsf(bf_hi(p[0]))), fmaxf(fabsf(bf_lo(p[1])), fabsf(bf_hi(p[1]))));
+}
+
+// PgFusedArgs.amax_zero: the first workgroup clears amax_zero[0 .. n) (a later launch's amax_out)
+__device__ __forceinline__ void amax_clear(const EpiArgs& e) {
+  if (e.f.amax_zero && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < e.f.amax_zero_n; i += blockDim.x) e.f.amax_zero[i] = 0u;
+}
+
 // --------------------------------------------------------------------------------------
 // Tiled GEMM (prefill)
 // --------------------------------------------------------------------------------------
@@ -302,7 +329,7 @@ __device__ __forceinline__ size_t frag_off(int row, int k0, int c, int K) {
 
 // Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread evenly over NW staging waves (wave < NW; others issue none).
 // FRAG: src is fragment-packed (ld = K); each piece still reads 8 runs of 128 contiguous bytes.
-template <int ROWS, bool FRAG = false, int NW = 4>
+template <int ROWS, bool FRAG = false, int NW = 4, int AUX = 0>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int rows_valid,
                                            int k0, char* lds_tile, int wave, int lane) {
   static_assert((ROWS / 8) % NW == 0, "pieces must split evenly over the staging waves");
@@ -316,7 +343,7 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int l
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
     const bf16_t* g = FRAG ? src + frag_off(gr, k0, c, ld) : src + (size_t)gr * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (LDS_AS void*)(lds_tile + blk * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)g, (LDS_AS void*)(lds_tile + blk * 1024), 16, 0, AUX);
   }
 }
 
@@ -345,6 +372,9 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
   }
 }
 
+#ifndef PG_TILE_M1_WNT
+#define PG_TILE_M1_WNT 0  // PG_TILE_M1 grids: stage W non-temporal (each W tile read by one workgroup)
+#endif
 #ifndef PG_TILE_PROBE
 #define PG_TILE_PROBE 0   // tuning builds only: 1 = staging without MFMAs, 2 = MFMAs without staging (wrong results)
 #endif
@@ -357,7 +387,9 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
 // grid for the small-M prefill GEMMs whose 64 x 128 grid leaves most CUs idle, without a K split.
 // KSUB = 2: a stage holds two 64-k sub-tiles (K % 128 == 0), one barrier / vmcnt wait per 128 k: half the
 // per-k-step synchronisation of the latency-bound small-M tiles.
-template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN, int KSUB = 1>
+// WNT: the W pieces are staged non-temporal (aux 2): for grids where each W tile is read by ONE workgroup (PG_TILE_M1)
+template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN, int KSUB = 1,
+          bool WNT = false>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ W, int ldw, int K,
                                                                int kchunk, int tiles_m, int tiles_n, EpiArgs e) {
@@ -415,7 +447,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
     for (int u = 0; u < KSUB; ++u) {
       const int k0 = kbeg + (kt * KSUB + u) * TBK;
       stage_tile<BM, false, NWA>(A, lda, m0, e.M, k0, st + u * SUB_BYTES, wave, lane);
-      stage_tile<BN, FRAG, NWW>(W, ldw, n0, e.N, k0, st + u * SUB_BYTES + A_BYTES, wave, lane);
+      stage_tile<BN, FRAG, NWW, WNT ? 2 : 0>(W, ldw, n0, e.N, k0, st + u * SUB_BYTES + A_BYTES, wave, lane);
     }
   };
 #pragma unroll
@@ -1375,6 +1407,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16_t* __restrict__ A,
 template <int EPI, int NT, int MT, int DEPTH, int CPW>
 __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ X, int ldx,
                                                     const uint8_t* __restrict__ W, int K, EpiArgs e) {
+  amax_clear(e);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -1482,10 +1515,16 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 // chunks of a row XOR-swizzled by row through the source address), issued before the W stream; each wave then
 // streams its own W tiles DEPTH chunks deep and reads its x fragments from LDS.  No cross-wave reduction: every
 // wave runs the epilogue of its own tiles (bf16, gelu*up on gate/up pairs, fp32 slabs, float-atomic residual add).
-template <int EPI, int NTW, int MT, int DEPTH, int CPW>
+// XB (pro_mode 5): X is bf16 h [M][ldx elements] and row m's amax (amax_in, max-ed by the gate/up epilogue): each
+// thread loads 16-element pieces, divides by s[m] = amax / 448 and packs e4m3 (pg_quant_fp8's bytes) into the same
+// swizzled LDS layout -- the quantiser launch between gate/up and down is gone; x costs twice the bytes per
+// workgroup (bf16), all issued before the W stream.
+template <int EPI, int NTW, int MT, int DEPTH, int CPW, bool XB = false>
 __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__ X, int ldx,
                                                      const uint8_t* __restrict__ W, int K, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char xs8[];
+  static_assert(!XB || CPW > 0, "the bf16-x form needs a compile-time chunk count");
+  amax_clear(e);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -1499,7 +1538,19 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
   const int Kr = nch * 128;                        // bytes of one x row in LDS
   // 1. x rows [0, 16 MT) x bytes [128 c0, +Kr) into LDS by DMA: LDS byte o = row * Kr + 16 pc holds logical chunk
   //    pc ^ (row & 7) of the row (rows past M repeat row M-1: their outputs are never stored)
-  {
+  constexpr int XPT = XB ? MT * 16 * CPW * 8 / 256 : 1;   // XB: 16-element pieces per thread
+  u32x4 xh[XPT][2];
+  if constexpr (XB) {
+    const bf16_t* Xb = (const bf16_t*)X;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int ci = (int)threadIdx.x + i * 256;   // LDS chunk: row ci / (8 CPW), position pc
+      const int row = ci / (8 * CPW), pc = ci % (8 * CPW);
+      const bf16_t* src = Xb + (size_t)min(row, M - 1) * ldx + (size_t)c0 * 128 + (pc ^ (row & 7)) * 16;
+      xh[i][0] = *(const u32x4*)src;
+      xh[i][1] = *(const u32x4*)(src + 8);
+    }
+  } else {
     const int pieces = MT * 16 * Kr / 1024;        // 1 KiB each, dealt round-robin to the waves
     for (int pi = wave; pi < pieces; pi += 4) {
       const int o = pi * 1024 + lane * 16;
@@ -1536,6 +1587,23 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
     const int wl = (CPW > 0 ? min(DEPTH, CPW) : min(DEPTH, nch)) * NTW * 2;
     (void)my_pieces;
     wait_vm_n(wl);
+    if constexpr (XB) {
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int ci = (int)threadIdx.x + i * 256;
+        const int row = ci / (8 * CPW), pc = ci % (8 * CPW);
+        const float am = __uint_as_float(e.f.amax_in[(size_t)min(row, M - 1) * e.f.amax_ld]);
+        const float sc = am > 0.f ? am / 448.f : 1.f;
+        u32x4 w8;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            w8[2 * h + j] = pack_fp8x4(bf_lo(xh[i][h][2 * j]) / sc, bf_hi(xh[i][h][2 * j]) / sc,
+                                       bf_lo(xh[i][h][2 * j + 1]) / sc, bf_hi(xh[i][h][2 * j + 1]) / sc);
+        *(u32x4*)(xs8 + row * Kr + pc * 16) = w8;
+      }
+    }
     __syncthreads();
   }
   auto compute = [&](int j, const u32x4 (&wv)[NTW][2]) {
@@ -1578,20 +1646,60 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
     }
   }
   const int q = 4 * g;
+  float gam[MT];                                   // GELU_MUL with amax_out: this lane's max |h| per row tile
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
+    gam[mt] = 0.f;
+    if constexpr (XB) {
+      const float am = __uint_as_float(e.f.amax_in[(size_t)min(m, M - 1) * e.f.amax_ld]);
+      const float sa = am > 0.f ? am / 448.f : 1.f;
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+      for (int t = 0; t < NTW; ++t) {
+        const int n0 = (tile0 + t) * 16 + q;
+        if (m < e.M && n0 < e.N) acc[t][mt] *= sa * load4_guard(e.f.w_scale, n0, e.N);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+    }
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+      if (e.f.amax_out) {
 #pragma unroll
-      for (int t = 0; t < NTW; t += 2) epi_gelu_mul4(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]);
+        for (int t = 0; t < NTW; t += 2)
+          gam[mt] = fmaxf(gam[mt], epi_gelu_mul4_amax(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]));
+      } else {
+#pragma unroll
+        for (int t = 0; t < NTW; t += 2) epi_gelu_mul4(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]);
+      }
     } else if constexpr (EPI == PG_EPI_F32_ADD) {
 #pragma unroll
       for (int t = 0; t < NTW; ++t) epi_add4(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
     } else {
 #pragma unroll
       for (int t = 0; t < NTW; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    }
+  }
+  if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
+    if (e.f.amax_out) {                            // (uniform: every wave reaches the barrier)
+      // row max over the 4 column groups of a lane's row, then over the 4 waves in LDS: one atomic per row per
+      // workgroup (float bits of non-negative values order as unsigned)
+      __shared__ float sam[4][16 * MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float v = gam[mt];
+        v = fmaxf(v, __shfl_xor(v, 16, 64));
+        v = fmaxf(v, __shfl_xor(v, 32, 64));
+        if (g == 0) sam[wave][mt * 16 + r] = v;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < 16 * MT && (int)threadIdx.x < M) {
+        const float v = fmaxf(fmaxf(sam[0][threadIdx.x], sam[1][threadIdx.x]),
+                              fmaxf(sam[2][threadIdx.x], sam[3][threadIdx.x]));
+        if (v > 0.f)
+          __hip_atomic_fetch_max(e.f.amax_out + (size_t)threadIdx.x * e.f.amax_ld, __float_as_uint(v),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -1605,6 +1713,15 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
   const int per_z = (nch + ksplit - 1) / ksplit;
   const size_t lds = (size_t)MT * 16 * per_z * 128;
   const bool exact = nch % ksplit == 0;
+  if constexpr (EPI == PG_EPI_F32) {
+    if (e.f.pro_mode == 5) {                       // bf16 x quantised while staged (host: exact, 8 or 16 chunks)
+      if (per_z == 16)
+        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 16, true>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+      else
+        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 8, true>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+      return;
+    }
+  }
   if (exact && per_z == 16)
     hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
   else if (exact && per_z == 8)
@@ -1656,6 +1773,19 @@ static void launch_gemv8(const uint8_t* X, int ldx, const uint8_t* W, int K, int
   // the wide form (x once per workgroup in LDS, waves split N) when its grid still has >= 256 workgroups and a
   // split's x rows fit the LDS; the K-split form otherwise (q|k|v: 160 tiles; o_proj)
   const int per_z = ((K >> 7) + ksplit - 1) / ksplit;
+  if constexpr (EPI == PG_EPI_F32) {
+    if (e.f.pro_mode == 5) {                       // bf16 x: the wide form only (host checked the chunk count)
+      const int wgs2 = (tiles + 7) / 8 * ksplit;
+      if (e.M <= 16) {
+        if (wgs2 >= 256) launch_gemv8x_mt<EPI, 2, 1>(X, ldx, W, K, ksplit, e, st);
+        else launch_gemv8x_mt<EPI, 1, 1>(X, ldx, W, K, ksplit, e, st);
+      } else {
+        if (wgs2 >= 256) launch_gemv8x_mt<EPI, 2, 2>(X, ldx, W, K, ksplit, e, st);
+        else launch_gemv8x_mt<EPI, 1, 2>(X, ldx, W, K, ksplit, e, st);
+      }
+      return;
+    }
+  }
   if constexpr (EPI != PG_EPI_QKV_ROPE) {
     if (PG_GEMV8_WIDE && per_z * 128 <= 4096) {
       const int wgs2 = (tiles + 7) / 8 * ksplit, wgs1 = (tiles + 3) / 4 * ksplit;
@@ -1769,13 +1899,14 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
       // streams once and no 256-row tile is spent on an 8-row remainder (M = 264: 2 x 256 rows in gemm256)
       const int tiles_n = (e.N + TBN - 1) / TBN;
       const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
+      constexpr bool WNT = PG_TILE_M1_WNT;
       if (e.M <= 256)
-        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 256, 3, FRAG, false, PG_TILE_W256>), dim3(tiles_n, 1, ksplit),
-                           dim3(64 * PG_TILE_W256), 0, st, A, lda,
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 256, 3, FRAG, false, PG_TILE_W256, TBN, 1, WNT>),
+                           dim3(tiles_n, 1, ksplit), dim3(64 * PG_TILE_W256), 0, st, A, lda,
                            W, ldw, K, kchunk, 1, tiles_n, e);
       else
-        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 288, 3, FRAG, false, PG_TILE_W288>), dim3(tiles_n, 1, ksplit),
-                           dim3(64 * PG_TILE_W288), 0, st, A, lda,
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 288, 3, FRAG, false, PG_TILE_W288, TBN, 1, WNT>),
+                           dim3(tiles_n, 1, ksplit), dim3(64 * PG_TILE_W288), 0, st, A, lda,
                            W, ldw, K, kchunk, 1, tiles_n, e);
       return;
     }
@@ -1902,13 +2033,20 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
-  PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 4);
+  PG_REQUIRE(f.pro_mode >= 0 && f.pro_mode <= 5);
+  if (f.pro_mode == 5)
+    PG_REQUIRE(fp8 && frag && epi == PG_EPI_F32 && M <= 32 && f.amax_in && f.amax_ld >= 1 && A != nullptr &&
+               lda >= K && lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && K % 128 == 0 && (K / 128) % ksplit == 0 &&
+               (K / 128 / ksplit == 8 || K / 128 / ksplit == 16));
+  if (f.amax_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.amax_ld >= 1 &&
+                             ((K >> 7) + ksplit - 1) / ksplit * 128 <= 4096 && PG_GEMV8_WIDE);
+  if (f.amax_zero) PG_REQUIRE(fp8 && frag && f.amax_zero_n >= 0 && f.amax_zero_n <= 4096);
   if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
   // (M > 4 runs two 16-row tiles per workgroup: the per-row entries are loaded 16 per lane)
   if (f.pro_mode == 4) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&
                                   ((M <= 2 && f.ss_n <= 256 && (M == 1 || f.ss_n <= 128)) ||
                                    (M > 4 && M <= 16 && f.ss_n <= 64)));
-  if (f.pro_mode != 0) PG_REQUIRE(M <= 16);
+  if (f.pro_mode != 0 && f.pro_mode != 5) PG_REQUIRE(M <= 16);
   if (f.pro_mode == 1) PG_REQUIRE(ksplit == 1 && f.resid_in && f.norm_w && (f.nsplit == 0 || f.partials) && K % 4 == 0);
   if (f.pro_mode == 2)
     PG_REQUIRE(f.part_o && f.part_ml && f.head_dim > 0 && (K / ksplit) % f.head_dim == 0 && f.asplit > 0 &&
@@ -1927,14 +2065,14 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
   if (epi == PG_EPI_BF16_VT) PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
   if (M <= 16) PG_REQUIRE(K % 64 == 0);
-  else PG_REQUIRE(K % TBK == 0 && f.pro_mode == 0 && epi != PG_EPI_F32_FIN);
+  else PG_REQUIRE(K % TBK == 0 && (f.pro_mode == 0 || f.pro_mode == 5) && epi != PG_EPI_F32_FIN);
   const bf16_t* a = (const bf16_t*)A;
   const bf16_t* w = (const bf16_t*)W;
   if (fp8 && frag) {
     // fp8 weight-streaming GEMV (M <= 32): fp8 fragment-packed W (weights.frag_pack8), row-major e4m3 x
-    PG_REQUIRE(M <= 32 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && N % 16 == 0 && ldw == K &&
-               lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 &&
-               epi != PG_EPI_F32_FIN);
+    PG_REQUIRE(M <= 32 && (f.pro_mode == 0 || f.pro_mode == 5) && (f.a_scale || f.pro_mode == 5) && f.w_scale &&
+               K % 128 == 0 && N % 16 == 0 && ldw == K && lda >= K && (lda % 16 == 0 || f.pro_mode == 5) &&
+               ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && epi != PG_EPI_F32_FIN);
     const uint8_t* x8 = (const uint8_t*)A;
     const uint8_t* w8 = (const uint8_t*)W;
     switch (epi) {

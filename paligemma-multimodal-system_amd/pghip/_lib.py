@@ -26,7 +26,9 @@ class PgFusedArgs(C.Structure):
                 ("q_heads", C.c_int), ("fin_cnt", C.c_void_p), ("fin_resid", C.c_void_p), ("ss_out", C.c_void_p),
                 ("ss_in", C.c_void_p), ("ss_ld", C.c_int), ("ss_n", C.c_int), ("fin_x", C.c_void_p),
                 ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
-                ("slab_rows", C.c_int), ("kd", C.c_void_p), ("vd", C.c_void_p)]
+                ("slab_rows", C.c_int), ("kd", C.c_void_p), ("vd", C.c_void_p),
+                ("amax_out", C.c_void_p), ("amax_in", C.c_void_p), ("amax_ld", C.c_int), ("amax_zero", C.c_void_p),
+                ("amax_zero_n", C.c_int)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -75,7 +77,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 def source_hash(lib=None) -> str:

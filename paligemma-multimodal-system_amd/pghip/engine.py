@@ -126,6 +126,15 @@ class PaliGemmaEngine:
     # chained greedy decode (single rank): the argmax's final launch also writes the next step's input rows
     # (pg_argmax_embed), so a decode step starts at layer 0 with no embed launch (decode_state(sampler=...))
     CHAIN_EMBED = os.environ.get("PG_CHAIN_EMBED", "1") != "0"
+    # 17..32-row fp8 decode: the down GEMV quantises h itself from the row maxima the gate/up epilogue collects
+    # (ops.gemm8_hx) instead of the pg_quant_fp8 launch between them.  Same bytes either way; measured slower at
+    # pt-896 x32 (r4 timelines: down 10.0 -> 15.7 us with 16 slabs, 18.0 with 8; gate/up +1.2 us for the
+    # atomics; the quantiser it removes costs 7.3 us), so off
+    HQ_FUSED = os.environ.get("PG_HQ_FUSED", "0") != "0"
+    AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
+    # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
+    # doubles instead (pt-896: 16 slabs of 8 chunks, as many x bytes per workgroup as the 8-slab fp8 route)
+    HQ_CHUNKS = int(os.environ.get("PG_HQ_CHUNKS", "8"))
     # B > FUSE_MAX_B: split-KV attention and its merge in one launch (pg_attn_decode; 0 = split kernel + combine)
     DECODE_FUSED_ATTN = os.environ.get("PG_DECODE_FUSED", "1") != "0"
     FUSED_MIN_ROUNDS = int(os.environ.get("PG_FUSED_MIN_ROUNDS", "3"))   # ... used from this many rounds per split on
@@ -179,6 +188,8 @@ class PaliGemmaEngine:
                   ("down_proj (PG_SPLIT_DOWN)", self.split_down, w.inter, 8)]
         if self.TILE_M1:    # (a model too narrow for this split just skips the row-tile path, _tile_m1)
             checks.append(("batch-1 prefill down_proj (PG_M1_DOWN)", self.TILE_M1_SPLIT["down"], 64 * 64, 64))
+        if self.HQ_CHUNKS not in (8, 16):
+            raise ValueError(f"PG_HQ_CHUNKS {self.HQ_CHUNKS}: the bf16-h down GEMV stages 8 or 16 chunks")
         for what, ks, K, hi in checks:          # (a split past K's 64-wide chunks just computes a zero slab)
             if not 1 <= ks <= hi:
                 raise ValueError(f"split-K {ks} for {what}: needs 1 <= split <= {hi} (K = {K})")
@@ -568,7 +579,7 @@ class PaliGemmaEngine:
         qb = self._buf("d_q", (B, nh * hd), torch.bfloat16)
         h = self._buf("d_h", (B, I), torch.bfloat16)
         so, sd = self._split_o(B), self.split_down
-        part = self._buf("d_part", (max(so, sd), B, H), torch.float32)
+        part = self._buf("d_part", (max(so, sd, 16), B, H), torch.float32)     # (16: the gemm8_hx down path)
         SK = self._split_keys(B, cache.Smax)
         nsplit = _rup((cache.Smax + SK - 1) // SK, 4)
         dt = (hd + 15) // 16 * 16
@@ -800,12 +811,24 @@ class PaliGemmaEngine:
         # x32 (down 11.5 -> 14.9 us: the MFMA output layout scatters each atomic instruction over 16 rows), so off
         add = (self.tp == 1 and self.DECODE_ADD_B32 and self.FP8_GEMV and self._fp8_rows(B) and B <= 32
                and "o_w8f" in w.tl[0] and "down_w8f" in w.tl[0])
+        # 17..32 rows on the fp8 GEMVs: the gate/up epilogue max-es each row's |h| (amax_out) and the down GEMV
+        # quantises h while staging it (ops.gemm8_hx) -- no quantiser launch; the QKV GEMV clears the maxima
+        ich = h.shape[1] // 128
+        sdh = ich // self.HQ_CHUNKS                # the down GEMV's splits on this path (x chunk per workgroup)
+        hq = (self.HQ_FUSED and self.FP8_GEMV and self._fp8_rows(B) and B <= 32 and not add
+              and all(k in w.tl[0] for k in ("qkv_w8f", "gu_w8f", "down_w8f"))
+              and ich % self.HQ_CHUNKS == 0 and part.shape[0] >= sdh)
+        if hq:
+            amax = self._buf("d_hamax", (B * self.AMAX_LD,), torch.int32)
+            fa_gu = ops.fused_args(amax_out=amax, amax_ld=self.AMAX_LD)
         ns = 0
         for i, Lw in enumerate(w.tl):
             xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
+            if hq:
+                fa.amax_zero, fa.amax_zero_n = amax.data_ptr(), B * self.AMAX_LD
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             a8 = self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS,
                                           nsplit, want_fp8=self._fp8_rows(B))
@@ -816,6 +839,11 @@ class PaliGemmaEngine:
                 self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
                 n_o = self._allreduce_slabs(part, so)
             xin = self._norm(res, Lw["post_w"], part, n_o, xn, B)
+            if hq:
+                self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B, fa=fa_gu)
+                ops.gemm8_hx(h, amax, self.AMAX_LD, Lw["down_w8f"], Lw["down_s8"], part, M=B, ksplit=sdh)
+                ns = self._allreduce_slabs(part, sdh)
+                continue
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
             if add:
                 self._lin(h, Lw, "down", res, ops.EPI_F32_ADD, B, ksplit=sd)

@@ -141,6 +141,26 @@ def gemm8(A8: torch.Tensor, a_scale: torch.Tensor, W8: torch.Tensor, w_scale: to
     return out
 
 
+def gemm8_hx(H: torch.Tensor, amax: torch.Tensor, amax_ld: int, W8: torch.Tensor, w_scale: torch.Tensor,
+             out: torch.Tensor, *, M: int, ksplit: int, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The fp8 GEMV (fragment-packed W8, EPI_F32 slabs) on bf16 rows H quantised in its prologue (pro_mode 5):
+    row m's scale is amax[m * amax_ld] (float bits of max |H[m]|, max-ed by a gemm8 gelu*up launch with
+    amax_out) / 448 -- the bytes and scale quant_fp8(H) would give, without its launch.  K / 128 / ksplit must be
+    8 or 16."""
+    _chk(H, torch.bfloat16, "H")
+    _chk(w_scale, torch.float32, "w_scale")
+    if W8.dtype != torch.uint8 or not W8.is_cuda or amax.dtype != torch.int32 or not amax.is_cuda:
+        raise ValueError("pghip.gemm8_hx: W8 uint8 (fragment-packed e4m3) and amax int32 HIP tensors")
+    N, K = W8.shape
+    if M > 32 or (K // 128) % ksplit or (K // 128 // ksplit) not in (8, 16) or amax.numel() < M * amax_ld:
+        raise ValueError("pghip.gemm8_hx: M <= 32, K / 128 / ksplit in (8, 16), amax [M * amax_ld]")
+    fa = fused_args(pro_mode=5, amax_in=amax, amax_ld=amax_ld, w_scale=w_scale)
+    ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
+    _lib.call("pg_gemm_fused", _p(H), H.stride(0), _p(W8), W8.stride(0), _p(bias), _p(out), ldc, M, N, K,
+              EPI_F32 | EPI_FP8 | W_FRAG, ksplit, _lib.C.byref(fa), _s())
+    return out
+
+
 def fused_args(**kw) -> "_lib.PgFusedArgs":
     """Build a PgFusedArgs; tensors are passed as their data pointers."""
     fa = _lib.PgFusedArgs()
@@ -264,6 +284,12 @@ def decode_plan(B: int, Hkv: int, kcap: int):
     return nsplit, nw, nb
 
 
+# the staggered form of pg_attn_decode (PG_ATTN_PIPE flag on nw; head_dim 256, 4-wave splits, >= 2 rounds): the
+# next block's K / V are issued between the current block's score and P.V phases
+ATTN_PIPE = os.environ.get("PG_ATTN_PIPE", "1") != "0"
+_ATTN_PIPE_FLAG = 0x100
+
+
 def attn_decode(q, q_rs, o, o_rs, kd, vd, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale, kcap, part_o, part_ml, counters,
                 plan=None, q8=None, q8_scale=None):
     """Batched decode attention with the split merge in the same launch (pg_attn_decode): o[b][hq*D + d] bf16 from
@@ -281,7 +307,7 @@ def attn_decode(q, q_rs, o, o_rs, kd, vd, *, B, Lkv, lkv_dev, Hq, Hkv, D, scale,
     if counters.dtype != torch.int32 or counters.numel() < B * Hkv:
         raise ValueError("pghip.attn_decode: counters must be int32 [B*Hkv]")
     _lib.call("pg_attn_decode", _p(q), q_rs, _p(o), o_rs, _p(kd), _p(vd), B, Lkv, _p(lkv_dev), Hq, Hkv, D,
-              float(scale), kcap, nsplit, nw, nb, _p(part_o), _p(part_ml), _p(counters), _p(q8), _p(q8_scale),
+              float(scale), kcap, nsplit, nw | (_ATTN_PIPE_FLAG if ATTN_PIPE else 0), nb, _p(part_o), _p(part_ml), _p(counters), _p(q8), _p(q8_scale),
               q8.stride(0) if q8 is not None else 0, _s())
 
 

@@ -368,7 +368,8 @@ def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
     cached keys; rows past L hold finite stale values (the static cache after a longer request), every split plan
     (2 / 4 waves, 1..16 splits, several rounds) agrees, repeated calls are bit-identical and leave the tickets zero.
     Where the plan allows it (one kv head, 4 waves) the second call also writes the fp8 row copy, which must equal
-    pg_quant_fp8 of the bf16 output byte for byte (ABI 7)."""
+    pg_quant_fp8 of the bf16 output byte for byte (ABI 7).  The staggered form (PG_ATTN_PIPE: next block's loads
+    between the phases, contiguous per-split block ranges) is bit-identical to the plain one."""
     from pghip import ops
     kvd = nkv * hd
     q = rnd(B, nh * hd, seed=31)
@@ -396,16 +397,21 @@ def test_attn_decode_fused(B, L, nh, nkv, hd, kcap):
         q8ok = ops.attn_decode_q8_ok(nh, nkv, hd, plan[1])
         q8 = torch.full((B, nh * hd), 0x55, dtype=torch.uint8, device="cuda")
         q8s = torch.zeros(B, device="cuda")
-        for rep in range(2):
-            ops.attn_decode(q, nh * hd, o, nh * hd, kd, vd,
-                            B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=kcap, part_o=po,
-                            part_ml=pml, counters=cnt, plan=plan, q8=q8 if rep and q8ok else None,
-                            q8_scale=q8s if rep and q8ok else None)
-            torch.cuda.synchronize()
-            assert int(cnt.abs().sum()) == 0, plan
-            if rep == 0:
-                first = o.clone()
-        assert torch.equal(first, o), plan
+        saved = ops.ATTN_PIPE
+        try:
+            for rep in range(3):
+                ops.ATTN_PIPE = rep != 2
+                ops.attn_decode(q, nh * hd, o, nh * hd, kd, vd,
+                                B=B, Lkv=1, lkv_dev=lkv, Hq=nh, Hkv=nkv, D=hd, scale=hd ** -0.5, kcap=kcap, part_o=po,
+                                part_ml=pml, counters=cnt, plan=plan, q8=q8 if rep == 1 and q8ok else None,
+                                q8_scale=q8s if rep == 1 and q8ok else None)
+                torch.cuda.synchronize()
+                assert int(cnt.abs().sum()) == 0, plan
+                if rep == 0:
+                    first = o.clone()
+                assert torch.equal(first, o), (plan, rep)
+        finally:
+            ops.ATTN_PIPE = saved
         if q8ok:
             r8, rs = ops.quant_fp8(o)
             assert torch.equal(q8, r8) and torch.equal(q8s, rs), plan
@@ -816,7 +822,7 @@ def _deq(q, s):
     return q.view(torch.float8_e4m3fn).float() * s[:, None]
 
 
-@pytest.mark.parametrize("M,K", [(1, 8), (7, 2048), (300, 16384), (64, 1152)])
+@pytest.mark.parametrize("M,K", [(1, 8), (7, 2048), (300, 16384), (64, 1152), (32, 16384), (3, 24576), (2, 40960)])
 def test_quant_fp8_rows_bit_identical_to_host_rule(M, K):
     """pg_quant_fp8 (row absmax / 448 scale, RNE e4m3) gives the same bytes and scales as the host rule the
     weights use (weights.quant_rows_fp8), including an all-zero row (scale 1)."""
@@ -916,3 +922,46 @@ def test_gemv8_fragment_packed_matches_the_fp8_tile_gemm(M, N, K, ks):
         g = ref.view(M, N // 32, 2, 16)
         want = (torch.nn.functional.gelu(g[:, :, 0], approximate="tanh") * g[:, :, 1]).reshape(M, N // 2)
         assert err(h, want) < 1e-2
+
+
+@pytest.mark.parametrize("M,I,H,ks", [(32, 16384, 2048, 8), (17, 4096, 1024, 2), (24, 2048, 512, 1), (9, 4096, 512, 2)])
+def test_gemm8_hx_equals_the_quantiser_route(M, I, H, ks):
+    """The batched fp8 decode MLP without pg_quant_fp8 (ABI 9): the gate/up GEMV max-es each row's |h| into
+    amax_out, the down GEMV (pro_mode 5, ops.gemm8_hx) quantises bf16 h while staging it.  h, the row maxima
+    (448 x quant_fp8's scales) and the down slabs are bit-identical to gate/up -> quant_fp8 -> gemm8; another fp8
+    GEMV launch's amax_zero clears stale maxima first (the engine's QKV GEMV)."""
+    from pghip import ops
+    from pghip.weights import frag_pack8, quant_rows_fp8
+    x = rnd(M, H, seed=81)
+    Wgu, Wd = rnd(2 * I, H, scale=1 / math.sqrt(H), seed=82), rnd(H, I, scale=1 / math.sqrt(I), seed=83)
+    x8, xs = ops.quant_fp8(x)
+    gu8, gus = quant_rows_fp8(Wgu)
+    d8, ds = quant_rows_fp8(Wd)
+    gu8f, d8f = frag_pack8(gu8), frag_pack8(d8)
+    ld = 32
+    amax = torch.full((M * ld,), 0x7F000000, dtype=torch.int32, device="cuda")     # stale maxima
+    w0, s0 = quant_rows_fp8(rnd(16, H, seed=84))
+    tmp = torch.empty(M, 16, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(x8, xs, frag_pack8(w0), s0, tmp, epi=ops.EPI_BF16, frag=True,
+              fa=ops.fused_args(amax_zero=amax, amax_zero_n=M * ld))
+    torch.cuda.synchronize()
+    assert int(amax.abs().sum()) == 0
+    h1 = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(x8, xs, gu8f, gus, h1, epi=ops.EPI_BF16_GELU_MUL, frag=True,
+              fa=ops.fused_args(amax_out=amax, amax_ld=ld))
+    h0 = torch.empty_like(h1)
+    ops.gemm8(x8, xs, gu8f, gus, h0, epi=ops.EPI_BF16_GELU_MUL, frag=True)
+    assert torch.equal(h0, h1)
+    h8, hs = ops.quant_fp8(h0)
+    got = amax.view(M, ld)[:, 0].view(torch.float32)
+    assert torch.equal(got, h0.float().abs().amax(1))   # (the scale amax / 448 is divided in-kernel: torch's
+    assert torch.allclose(got / 448, hs, rtol=1e-6, atol=0)  # tensor / scalar multiplies by the reciprocal)
+    p0 = torch.empty(ks, M, H, dtype=torch.float32, device="cuda")
+    p1 = torch.empty_like(p0)
+    ops.gemm8(h8, hs, d8f, ds, p0, epi=ops.EPI_F32, ksplit=ks, frag=True)
+    ops.gemm8_hx(h0, amax, ld, d8f, ds, p1, M=M, ksplit=ks)
+    torch.cuda.synchronize()
+    if (H // 16 + 3) // 4 * ks >= 256:       # the quantiser route also ran the wide form: the same sums
+        assert torch.equal(p0, p1)
+    else:                                    # it ran the K-split form: fp32 summation order differs
+        assert torch.allclose(p0, p1, rtol=1e-5, atol=1e-5)
