@@ -1704,7 +1704,7 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
   }
 }
 
-template <int EPI, int NTW, int MT>
+template <int EPI, int NTW, int MT, int DEPTH = 8>
 static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                              hipStream_t st) {
   const int tiles = e.N >> 4;
@@ -1723,11 +1723,11 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
     }
   }
   if (exact && per_z == 16)
-    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
   else if (exact && per_z == 8)
-    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 8>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 8>), grid, dim3(256), lds, st, X, ldx, W, K, e);
   else
-    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, 8, 0>), grid, dim3(256), lds, st, X, ldx, W, K, e);
+    hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 0>), grid, dim3(256), lds, st, X, ldx, W, K, e);
 }
 
 #ifndef PG_GEMV8_DEPTH

@@ -131,6 +131,7 @@ class PaliGemmaEngine:
     # pt-896 x32 (r4 timelines: down 10.0 -> 15.7 us with 16 slabs, 18.0 with 8; gate/up +1.2 us for the
     # atomics; the quantiser it removes costs 7.3 us), so off
     HQ_FUSED = os.environ.get("PG_HQ_FUSED", "0") != "0"
+
     AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
     # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
     # doubles instead (pt-896: 16 slabs of 8 chunks, as many x bytes per workgroup as the 8-slab fp8 route)
@@ -318,7 +319,7 @@ class PaliGemmaEngine:
                                 kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax, q_heads=nh, kv_heads=nkv,
                                 kd=cache.kd[i], vd=cache.vd[i])
             self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, T, fa=fa)
-            ops.attention(qb, nh * hd, attn, nh * hd, cache.k[i], cache.Smax * kvd, hd, kvd,
+            ops.attention(qb, nh * hd, attn, attn.stride(0), cache.k[i], cache.Smax * kvd, hd, kvd,
                           cache.vt[i], kvd * cache.Smax, hd * cache.Smax, cache.Smax,
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
