@@ -329,7 +329,9 @@ __device__ __forceinline__ size_t frag_off(int row, int k0, int c, int K) {
 
 // Stage a ROWS x 64-k bf16 tile: ROWS/8 pieces spread evenly over NW staging waves (wave < NW; others issue none).
 // FRAG: src is fragment-packed (ld = K); each piece still reads 8 runs of 128 contiguous bytes.
-template <int ROWS, bool FRAG = false, int NW = 4, int AUX = 0>
+// SKIP: pieces whose 8 rows all lie past rows_valid are not loaded (their LDS rows feed only outputs that are never
+// stored); the caller counts the pieces a wave issues with stage_pieces.
+template <int ROWS, bool FRAG = false, int NW = 4, int AUX = 0, bool SKIP = false>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int ld, int row0, int rows_valid,
                                            int k0, char* lds_tile, int wave, int lane) {
   static_assert((ROWS / 8) % NW == 0, "pieces must split evenly over the staging waves");
@@ -338,6 +340,7 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int l
 #pragma unroll
   for (int it = 0; it < PER_WAVE; ++it) {
     const int blk = wave * PER_WAVE + it;          // 1 KiB piece = 8 rows x 128 B
+    if (SKIP && blk * 8 >= rows_valid - row0) break;   // (wave-uniform)
     const int r = blk * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((r >> 1) & 7);     // logical 16-B chunk landing at physical chunk lane&7
     int gr = row0 + r;
@@ -345,6 +348,16 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ src, int l
     const bf16_t* g = FRAG ? src + frag_off(gr, k0, c, ld) : src + (size_t)gr * ld + k0 + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)g, (LDS_AS void*)(lds_tile + blk * 1024), 16, 0, AUX);
   }
+}
+
+// pieces stage_tile<ROWS, *, NW, *, SKIP> issues for this wave
+template <int ROWS, int NW, bool SKIP>
+__device__ __forceinline__ int stage_pieces(int row0, int rows_valid, int wave) {
+  constexpr int PER_WAVE = ROWS / 8 / NW;
+  if (wave >= NW) return 0;
+  if (!SKIP) return PER_WAVE;
+  const int valid = (rows_valid - row0 + 7) / 8;
+  return min(PER_WAVE, max(0, valid - wave * PER_WAVE));
 }
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int row, int chunk) {
@@ -411,8 +424,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   // an exec-masked chain of every case
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
-  // glds pieces this wave issues per stage (wave-uniform): its vmcnt step per younger stage in flight
-  const int P = KSUB * (BM / 8 / NWA + (wave < NWW ? BN / 8 / NWW : 0));
 
   // XCD-aware bijective remap (blocks b and b+8 share an XCD), then grouped tile order.
   const int nwg = gridDim.x;
@@ -428,6 +439,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   const int tm = first_m + (pid % gsize);
   const int tn = (pid % (GROUP * tiles_n)) / gsize;
   const int m0 = tm * BM, n0 = tn * BN;
+  // glds pieces this wave issues per stage (wave-uniform): its vmcnt step per younger stage in flight; A pieces of
+  // padding rows only (the last row tile: M = 264 in a 288-row tile) are not loaded
+  const int P = KSUB * (stage_pieces<BM, NWA, true>(m0, e.M, wave) + stage_pieces<BN, NWW, false>(n0, e.N, wave));
 
   const int z = blockIdx.z;
   const int kbeg = z * kchunk;
@@ -446,7 +460,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 #pragma unroll
     for (int u = 0; u < KSUB; ++u) {
       const int k0 = kbeg + (kt * KSUB + u) * TBK;
-      stage_tile<BM, false, NWA>(A, lda, m0, e.M, k0, st + u * SUB_BYTES, wave, lane);
+      stage_tile<BM, false, NWA, 0, true>(A, lda, m0, e.M, k0, st + u * SUB_BYTES, wave, lane);
       stage_tile<BN, FRAG, NWW, WNT ? 2 : 0>(W, ldw, n0, e.N, k0, st + u * SUB_BYTES + A_BYTES, wave, lane);
     }
   };
