@@ -1072,7 +1072,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   // own row, so the row total is a reduction over the 4 lane groups
   // (one-tile workgroups at M > 4 -- the batched q|k|v, launch_gemv_pro -- use the same 16-entry layout as the
   // two-tile form)
-  constexpr bool SS16 = PRO == 4 && (NT == 2 || EPI == PG_EPI_QKV_ROPE);
+  constexpr bool SS16 = PRO == 4 && (NT >= 2 || EPI == PG_EPI_QKV_ROPE);
   constexpr int SSL = SS16 ? 16 : 4;
   float ssv[SSL];
 #pragma unroll
@@ -1282,6 +1282,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     // The reducer reads the slabs with sc1 loads (bypass its L1/L2), so no acquire fence either.
     const PgFusedArgs& f = e.f;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
+    // one sum-of-squares entry per tile pair (per tile at NT 1): a 4-tile workgroup writes two
+    constexpr int SE = NT >= 2 ? NT / 2 : 1;
     auto finish = [&](int t, int n0, f32x4 v, float& ssl) {   // v = the finalised residual of (m, n0..n0+3)
       *(f32x4*)(f.fin_resid + (size_t)m * e.N + n0) = v;
       ssl += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
@@ -1293,23 +1295,27 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
         *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
       }
     };
-    auto put_ss = [&](float ssl) {
-      if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx] = ssl;
+    auto put_ss = [&](float (&ssl)[SE]) {
+#pragma unroll
+      for (int p = 0; p < SE; ++p) {
+        const float v = sum_xor32(sum_xor16(ssl[p]));
+        if (g == 0 && m < M) f.ss_out[(size_t)m * f.ss_ld + gi.bx * SE + p] = v;
+      }
     };
     if (gi.ny == 1) {
       // no split: this workgroup owns the tile -- no slab, no ticket (same sums: residual + (acc + bias))
-      float ssl = 0.f;
+      float ssl[SE];
+#pragma unroll
+      for (int p = 0; p < SE; ++p) ssl[p] = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int n0 = (tile0 + t) * 16 + q;
         if (m < M && n0 < e.N) {
           f32x4 v = acc[t];
           if (e.bias) v += load4_guard(e.bias, n0, e.N);
-          finish(t, n0, fin_r[t] + v, ssl);
+          finish(t, n0, fin_r[t] + v, ssl[t / 2 < SE ? t / 2 : 0]);
         }
       }
-      ssl = sum_xor16(ssl);
-      ssl = sum_xor32(ssl);
       put_ss(ssl);
       return;
     }
@@ -1332,7 +1338,9 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     old = __shfl(old, 0, 64);
     if (old != gi.ny - 1) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // compiler-only: keep the loads below the ticket
-    float ssl = 0.f;
+    float ssl[SE];
+#pragma unroll
+    for (int p = 0; p < SE; ++p) ssl[p] = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = (tile0 + t) * 16 + q;
@@ -1353,11 +1361,9 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
                             __uint_as_float(sb[zz][1])};
           v += zz < Z ? sv : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        finish(t, n0, v, ssl);
+        finish(t, n0, v, ssl[t / 2 < SE ? t / 2 : 0]);
       }
     }
-    ssl = sum_xor16(ssl);
-    ssl = sum_xor32(ssl);
     put_ss(ssl);
     if (lane == 0) __hip_atomic_store(f.fin_cnt + gi.bx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1382,7 +1388,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     return;
   }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
-    epi_gelu_mul4(e, m, tile0 * 16, q, acc[0], acc[1]);
+#pragma unroll
+    for (int t = 0; t < NT; t += 2) epi_gelu_mul4(e, m, (tile0 + t) * 16, q, acc[t], acc[t + 1]);
   } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -1991,6 +1998,8 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
       return;
     }
   }
+  // (four tiles per workgroup at 5..16 rows -- x's share of a workgroup's bytes 1/5 instead of 1/3 -- measured
+  // slower on the pt-448 x16 gate/up and finalised down: 1.408 vs 1.380 ms/step; the epilogues take any even NT)
   // ring depths re-checked on the final round-2 code: two-tile kernels 4 chunks in flight, one-tile 8
   if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
     launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(dim3((ntiles + 1) / 2, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);

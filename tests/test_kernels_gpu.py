@@ -965,3 +965,31 @@ def test_gemm8_hx_equals_the_quantiser_route(M, I, H, ks):
         assert torch.equal(p0, p1)
     else:                                    # it ran the K-split form: fp32 summation order differs
         assert torch.allclose(p0, p1, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("M,N,K,ks", [(16, 2048, 16384, 8), (16, 2048, 2048, 2), (8, 1024, 4096, 4), (16, 512, 1024, 1)])
+def test_gemv_fin_residual_xprime_and_pair_sums(M, N, K, ks):
+    """PG_EPI_F32_FIN on the bf16 GEMV (5..16-row decode): the residual += x.W^T (+ bias) finalised in-kernel, x' =
+    bf16(resid * (1 + w)) and one sum of squares per 32-column tile pair -- at the shapes that run 4 tiles per
+    workgroup (N 2048 x 8 splits: the pt-448 x16 down projection) and the 2-tile ones; the tickets are left zero."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    tiles = N // 16
+    x, W = rnd(M, K, seed=91), rnd(N, K, scale=1 / math.sqrt(K), seed=92)
+    bias = torch.randn(N).cuda() * 0.1
+    resid0 = torch.randn(M, N).cuda()
+    norm_w = torch.randn(N).cuda() * 0.1
+    res = resid0.clone()
+    cnt = torch.zeros(tiles, dtype=torch.int32, device="cuda")
+    ss = torch.full((M, tiles), -1.0, device="cuda")
+    xq = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    part = torch.empty(ks, M, N, dtype=torch.float32, device="cuda")
+    fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss, ss_ld=tiles, fin_x=xq, norm_w=norm_w)
+    ops.gemm_fused(x, frag_pack(W), part, fa, epi=ops.EPI_F32_FIN | ops.W_FRAG, M=M, ksplit=ks, bias=bias)
+    torch.cuda.synchronize()
+    ref = resid0 + x.float() @ W.float().t() + bias
+    assert err(res, ref) < 1e-4
+    assert err(xq, ref * (1 + norm_w)) < 1e-2
+    pairs = (ref * ref).view(M, tiles // 2, 32).sum(-1)
+    assert torch.allclose(ss[:, :tiles // 2], pairs, rtol=1e-4, atol=1e-3)
+    assert int(cnt.abs().sum()) == 0
