@@ -586,13 +586,21 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
       const int blk = wave * 2 + it;                 // 16 pieces of 8 rows x 128 B
       const int r = blk * 8 + (lane >> 3);           // half-image row
       const int c = (lane & 7) ^ ((r >> 1) & 7);
-      const bf16_t* src;
+      // fp8: uniform base + 32-bit per-lane byte offset (the host checks both operands are < 4 GiB): the saddr
+      // form, one VGPR per piece instead of a 64-bit pointer (the fp8 instance spilled its hoisted piece pointers)
+      const char* src;
       if (h < 2) {
         const int gr = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), e.M - 1);
-        src = A + (size_t)gr * lda + k0 + c * 8;
+        if constexpr (F8)
+          src = (const char*)A + (uint32_t)(((unsigned)gr * (unsigned)lda + (unsigned)(k0 + c * 8)) * 2u);
+        else
+          src = (const char*)(A + (size_t)gr * lda + k0 + c * 8);
       } else {
         const int gn = min(n0 + (r >> 5) * 64 + (h - 2) * 32 + (r & 31), e.N - 1);
-        src = FRAG ? W + frag_off(gn, k0, c, ldw) : W + (size_t)gn * ldw + k0 + c * 8;
+        if constexpr (F8 && !FRAG)
+          src = (const char*)W + (uint32_t)(((unsigned)gn * (unsigned)ldw + (unsigned)(k0 + c * 8)) * 2u);
+        else
+          src = (const char*)(FRAG ? W + frag_off(gn, k0, c, ldw) : W + (size_t)gn * ldw + k0 + c * 8);
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + blk * 1024), 16, 0, 0);
     }
@@ -814,7 +822,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #define PG_GEMV_CONTIG 0
 #endif
 #ifndef PG_F8_G256
-#define PG_F8_G256 0            // fp8 GEMMs on the 256x256 kernel: it spills at fp8 (2x slower than the 128x128 tile kernel)
+// fp8 GEMMs on the 256x256 kernel: 0 never, 1 the fp32-slab epilogue only (pt-896 x32 o + down 115.7 -> 102.5 ms per
+// prefill), 2 every epilogue (gate/up 182 -> 211 ms and q|k|v 21 -> 48 ms: those instances still spill)
+#define PG_F8_G256 1
 #endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
@@ -1933,7 +1943,10 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
     }
   }
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
-  if ((PG_F8_G256 || !F8) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
+  // (fp8 on the 256 x 256 kernel addresses its operands by 32-bit byte offsets: both must be < 4 GiB)
+  const bool off32 = (size_t)e.M * lda * 2 < (1ull << 32) && (size_t)e.N * ldw * 2 < (1ull << 32);
+  constexpr bool g256 = !F8 || PG_F8_G256 == 2 || (PG_F8_G256 == 1 && EPI == PG_EPI_F32);
+  if (g256 && (!F8 || off32) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;
     hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG, F8>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
                        (e.M + 255) / 256, (e.N + 255) / 256, e);
