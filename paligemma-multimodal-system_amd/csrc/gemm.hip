@@ -821,6 +821,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_CONTIG
 #define PG_GEMV_CONTIG 0
 #endif
+#ifndef PG_T128_STAGES_F8
+#define PG_T128_STAGES_F8 2  // stages of the 128 x 128 fp8 tile (2: two workgroups per CU; 3 / 4 = one per CU, pt-896 x32
+                             // gate/up 10.1 -> 14.6 / 14.3 ms)
+#endif
 #ifndef PG_F8_G256
 // fp8 GEMMs on the 256x256 kernel: 0 never, 1 the fp32-slab epilogue only (pt-896 x32 o + down 115.7 -> 102.5 ms per
 // prefill), 2 every epilogue (gate/up 182 -> 211 ms and q|k|v 21 -> 48 ms: those instances still spill)
@@ -1957,7 +1961,8 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   const int t128 = ((e.M + 127) / 128) * tiles_n;
   if (t128 >= 256) {
     const int tiles_m = (e.M + 127) / 128;
-    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, 2, FRAG, F8, PG_TILE_W128>), dim3(tiles_m * tiles_n, 1, ksplit),
+    hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, F8 ? PG_T128_STAGES_F8 : 2, FRAG, F8, PG_TILE_W128>),
+                       dim3(tiles_m * tiles_n, 1, ksplit),
                        dim3(64 * PG_TILE_W128), 0, st,
                        A, lda, W, ldw, K, kchunk, tiles_m, tiles_n, e);
     return;
