@@ -800,7 +800,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 // k = chunk + 8U*g; MFMA step s consumes k = chunk + 8U*g + 8s + [0,8) for BOTH operands, a
 // permutation of k that leaves the dot product unchanged.  DEPTH chunks stay in flight in a
 // statically indexed register ring.  Plain (temporal) loads: measured 1.2-1.6x faster than
-// non-temporal ones on every decode shape (scripts/tune/tune_gemv.py).
+// non-temporal ones on every decode shape (round-1 GEMV sweep).
 //
 // PRO (prologue, fuses the producer of x into the GEMV so a decode layer needs 5 launches):
 //   0: x rows read from A (bf16)
@@ -1978,7 +1978,7 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   launch_t64<EPI, FRAG, F8, TBN, PG_TILE_W64>(A, lda, W, ldw, K, ksplit, e, st);
 }
 
-// measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
+// measured configs (round-1 GEMV sweep): M <= 4: one tile per WG, U=2, 8 chunks in flight;
 // M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
 // one gemv_kernel launch with the chunks-per-wave specialisation when the K split is exact (see gemv_kernel)
 template <int EPI, int NT, int DEPTH, int PRO, bool FRAG>
@@ -1994,7 +1994,7 @@ static void launch_gemv_cpw(dim3 grid, size_t lds, hipStream_t st, const bf16_t*
   }
 }
 
-// measured configs (scripts/tune/tune_gemv.py): M <= 4: one tile per WG, U=2, 8 chunks in flight;
+// measured configs (round-1 GEMV sweep): M <= 4: one tile per WG, U=2, 8 chunks in flight;
 // M > 4 and the gate/up pair: two tiles per WG, U=2, 4 chunks in flight.
 template <int EPI, int PRO, bool FRAG>
 static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
