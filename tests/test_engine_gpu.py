@@ -334,3 +334,33 @@ def test_pt224_free_running_greedy_ids_equal_reference(golden):
     px = torch.from_numpy(np.concatenate(pvs)).cuda()
     got = eng.generate(ids, px, torch.ones_like(ids), len(want[0]), stop_token=None, use_graph=True)
     assert got.tolist() == want
+
+
+@pytest.mark.gpu
+def test_bench_prints_one_contract_json_line():
+    """bench.py (the driver's contract): one JSON line on stdout with the required keys, BASELINE.json's metric and
+    configs[1] workload, a roofline object with achieved / peak / frac consistent with each other, and a
+    cpu_baseline object from the oracle port on a bounded sample (here 2 steps after 1 warmup)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=280, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    o = json.loads(lines[0])
+    base = json.load(open(os.path.join(root, "BASELINE.json")))
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in o, k
+    assert o["metric"] == base["metric"] and o["n_gpus"] == 1 and o["steps"] == 2 and o["warmup"] == 1
+    assert o["value"] > 0 and o["higher_is_better"] is True and o["scaling"] == "weak" and o["dtype"] == "bf16"
+    assert "configs[1]" in o["config"]["workload"]
+    rf = o["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert 0 < rf["frac"] <= 1 and abs(rf["achieved"] / rf["peak"] - rf["frac"]) < 1e-3
+    cb = o["cpu_baseline"]
+    assert cb["kind"] in ("port", "reference") and cb["value"] and cb["value"] > 0 and cb["cores"] >= 1
