@@ -839,6 +839,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 #ifndef PG_GEMV_D2
 #define PG_GEMV_D2 4
 #endif
+#ifndef PG_GEMV_D1
+#define PG_GEMV_D1 8      // chunks in flight of the one-tile GEMV (M <= 4: batch-1 decode o / down / q|k|v / lm_head)
+#endif
 #ifndef PG_GEMV_XLDS
 #define PG_GEMV_XLDS 0
 #endif
@@ -2022,7 +2025,7 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   if (EPI == PG_EPI_BF16_GELU_MUL || e.M > 4) {
     launch_gemv_cpw<EPI, 2, PG_GEMV_D2, PRO, FRAG>(dim3((ntiles + 1) / 2, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   } else {
-    launch_gemv_cpw<EPI, 1, 8, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
+    launch_gemv_cpw<EPI, 1, PG_GEMV_D1, PRO, FRAG>(dim3(ntiles, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
   }
 }
 
