@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -45,6 +45,10 @@ enum {
   PG_EPI_F32_ADD = 8        /* (ABI 8) M <= 16, pro_mode 0 or 2: C f32 [M][ldc] += acc (+ bias by split 0) by
                                hardware float atomic adds in any split order (the residual add of gemma.py:401,416
                                with no slab or ticket; the next GEMV normalises with pro_mode 1, nsplit 0)       */
+  PG_EPI_FX_ADD = 9         /* (ABI 10) M <= 16, bf16, pro_mode 0 or 2: C int64 [M][ldc] += round(acc * 2^32) (+ bias by
+                               split 0) by 64-bit integer atomics -- F32_ADD's residual add, but the fixed-point sum is
+                               exact and so the same bits in any split order (bit-reproducible decode).  C is the
+                               PgFusedArgs.fx accumulator that pro_mode 1 and PG_EPI_F32_FIN consumers read      */
 };
 
 /* Fused-operation arguments of pg_gemm_fused (M <= 16 for the prologues). */
@@ -99,6 +103,11 @@ typedef struct PgFusedArgs {
   int amax_ld;
   unsigned* amax_zero;      /* optional, any PG_FP8|PG_W_FRAG launch: amax_zero[0 .. amax_zero_n) set to 0 (n <= 4096) */
   int amax_zero_n;
+  /* ABI 10: */
+  int64_t* fx;              /* fixed-point residual accumulator [M][K] (value = q * 2^-32, |value| < 2^31) written by
+                               PG_EPI_FX_ADD producers.  pro_mode 1: x = RMSNorm(resid_in + fx + sum partials) ;
+                               PG_EPI_F32_FIN (pro_mode != 1): the finalised residual is fin_resid + fx + slabs, and
+                               the launch leaves fx zero (each tile's finalising workgroup clears its entries)       */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,

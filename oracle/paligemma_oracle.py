@@ -47,12 +47,13 @@ class bf16_operands:
         _BF16_OPERANDS = self._old
 
 
-# fp8-operand emulation (test aid, BASELINE configs[4]): when on, the Gemma decoder linears (q/k/v/o, gate/up/down;
-# not the lm_head, which the HIP path keeps bf16) multiply e4m3 operands -- activation rows and weight output rows
-# each scaled by max|row| / 448 (weights.quant_rows_fp8 / pg_quant_fp8's rule) -- whenever a call has more than
-# `min_rows` rows (the HIP path runs fp8 for linears of more than 16 rows: prefill, and decode at batch > 16).
-# The fp8 path's intrinsic sensitivity on a model then bounds the HIP fp8 path's distance to the fp32 reference.
-# lm_head=True also runs the tied lm_head on e4m3 operands (the HIP path's batch > 16 decode lm_head).
+# fp8-operand emulation (test aid, BASELINE configs[4]): when on, the Gemma decoder linears (q/k/v/o, gate/up/down)
+# multiply e4m3 operands -- activation rows and weight output rows each scaled by max|row| / 448
+# (weights.quant_rows_fp8 / pg_quant_fp8's rule) -- whenever a call has more than `min_rows` rows (the HIP path runs
+# fp8 for linears of more than 16 rows: prefill, and decode at batch > 16).  The fp8 path's intrinsic sensitivity on a
+# model then bounds the HIP fp8 path's distance to the fp32 reference.  The tied lm_head: the HIP path runs it in e4m3
+# for 17..32-row batches (engine._lm_gemm, the fp8 GEMV) and in bf16 otherwise; lm_head=True emulates the e4m3 form
+# (tests/golden/make_emu.py sets it for the batch-32 fixtures).
 _FP8_MIN_ROWS = None
 _FP8_LM_HEAD = False
 

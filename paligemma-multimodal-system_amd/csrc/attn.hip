@@ -28,8 +28,8 @@
 #ifndef PG_COMBINE_PF
 #define PG_COMBINE_PF 12  // split-KV merge: O partials of the first 12 splits per thread loaded up front
 #endif
-#ifndef PG_ATTN_WG
 #define PG_ATTN_PIPE 0x100 // pg_attn_decode: flag OR-ed into nw -- the double-buffered form (include/pghip.h)
+#ifndef PG_ATTN_WG
 #define PG_ATTN_WG 1      // decode splits of 2 / 4 / 8 blocks (head_dim 256): one wave per block, merged in LDS
 #endif
 #ifndef PG_ATTN_SPLIT_WAVES

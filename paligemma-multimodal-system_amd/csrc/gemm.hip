@@ -44,7 +44,27 @@ enum {
                             // (ss_out): the residual add + RMSNorm statistics of the NEXT norm, done in-kernel
   PG_EPI_F32_ADD = 8,       // GEMV (M <= 16): C f32 [M][ldc] += acc (+ bias by split 0) with hardware float atomic
                             // adds, any split count (the residual add of a row-parallel decode linear, no slabs)
+  PG_EPI_FX_ADD = 9,        // GEMV (M <= 16, bf16): C int64 [M][ldc] += rn(acc * 2^32) (+ bias by split 0) with
+                            // 64-bit integer atomics: F32_ADD's one-round-trip tail, but the sum is exact and so
+                            // independent of the split order -- bit-reproducible decode (PgFusedArgs.fx)
 };
+
+// the fixed-point residual accumulator (PG_EPI_FX_ADD, PgFusedArgs.fx): value = q * 2^-32, |value| < 2^31
+#define PG_FX_SCALE 0x1p32f
+#define PG_FX_INV 0x1p-32f
+__device__ __forceinline__ long long fx_from_f32(float v) { return __float2ll_rn(v * PG_FX_SCALE); }
+// (consumers convert every entry of a row in every workgroup, so this is 3 VALU ops instead of __ll2float_rn's 12:
+// q = hi * 2^32 + lo with hi = q >> 32 (arithmetic), lo the unsigned low word; value = hi + lo * 2^-32, rounded twice --
+// a fixed function of q's bits, so every reader gets the same float)
+__device__ __forceinline__ float fx_to_f32(long long q) {
+  return fmaf((float)(unsigned)(unsigned long long)q, PG_FX_INV, (float)(int)(q >> 32));
+}
+typedef long long i64x2 __attribute__((ext_vector_type(2)));
+// 4 consecutive accumulator entries as fp32 (two 16-B loads)
+__device__ __forceinline__ f32x4 fx_load4(const long long* p) {
+  const i64x2 a = *(const i64x2*)p, b = *(const i64x2*)(p + 2);
+  return f32x4{fx_to_f32(a[0]), fx_to_f32(a[1]), fx_to_f32(b[0]), fx_to_f32(b[1])};
+}
 
 // Extra arguments of the fused entry point pg_gemm_fused (mirrors PgFusedArgs in include/pghip.h).
 struct PgFusedArgs {
@@ -99,6 +119,10 @@ struct PgFusedArgs {
   int amax_ld;
   unsigned* amax_zero;
   int amax_zero_n;
+  // ABI 10: the fixed-point residual accumulator [M][K] int64 (value q * 2^-32) that PG_EPI_FX_ADD producers add
+  // into.  pro_mode 1 normalises resid_in + fx (+ partials); PG_EPI_F32_FIN finalises fin_resid + fx + slabs and
+  // clears the fx entries it finalised (the accumulator is zero again once the FIN launch ends)
+  long long* fx;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -894,6 +918,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
         if (c < K4) {
           wn[i] = ((const f32x4*)f.norm_w)[c];          // issued with the residual: one round trip
           f32x4 a = ((const f32x4*)f.resid_in)[c];
+          if (f.fx) a += fx_load4(f.fx + 4 * c);
           for (int sp = 0; sp < f.nsplit; ++sp) a += ((const f32x4*)(f.partials + (size_t)sp * K))[c];
           v[i] = a;
           ss += a[0] * a[0] + a[1] * a[1] + a[2] * a[2] + a[3] * a[3];
@@ -922,6 +947,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
       float ss = 0.f;
       for (int c = t; c < K4; c += 256) {
         f32x4 v = ((const f32x4*)(f.resid_in + (size_t)m * K))[c];
+        if (f.fx) v += fx_load4(f.fx + (size_t)m * K + 4 * c);
         for (int sp = 0; sp < f.nsplit; ++sp) v += ((const f32x4*)(f.partials + ((size_t)sp * M + m) * K))[c];
         ss += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
         if (w0) ((f32x4*)(f.resid_out + (size_t)m * K))[c] = v;
@@ -934,6 +960,7 @@ __device__ __forceinline__ void gemv_prologue(const EpiArgs& e, int M, int K, in
       const float rstd = rsqrtf((red[m] + red[16 + m] + red[32 + m] + red[48 + m]) / (float)K + f.eps);
       for (int c = t; c < K4; c += 256) {
         f32x4 v = ((const f32x4*)(f.resid_in + (size_t)m * K))[c];
+        if (f.fx) v += fx_load4(f.fx + (size_t)m * K + 4 * c);
         for (int sp = 0; sp < f.nsplit; ++sp) v += ((const f32x4*)(f.partials + ((size_t)sp * M + m) * K))[c];
         const f32x4 w = ((const f32x4*)f.norm_w)[c];
         u32x2 pk;
@@ -1191,11 +1218,17 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
   // PG_EPI_F32_FIN: the residual rows and norm weights the tile's last-arriving split finalises are loaded now
   // (nothing else writes them in this launch), so the reducer's only round trip is the slab read
   f32x4 fin_r[NT], fin_w[NT];
+  i64x2 fin_fa[NT], fin_fb[NT];     // the fixed-point accumulator's entries (PgFusedArgs.fx), converted when used
   if constexpr (EPI == PG_EPI_F32_FIN) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = min((tile0 + t) * 16, e.N - 16) + 4 * g;
       fin_r[t] = *(const f32x4*)(e.f.fin_resid + (size_t)(r < M ? r : M - 1) * e.N + n0);
+      if (e.f.fx) {
+        const long long* p = e.f.fx + (size_t)(r < M ? r : M - 1) * e.N + n0;
+        fin_fa[t] = *(const i64x2*)p;
+        fin_fb[t] = *(const i64x2*)(p + 2);
+      }
       // (no select on a loaded value -- it would make the compiler wait right here: a null norm_w reads the
       // residual row instead, unused)
       fin_w[t] = *(const f32x4*)((e.f.norm_w ? e.f.norm_w : e.f.fin_resid) + n0);
@@ -1312,6 +1345,21 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
         *(u32x2*)(f.fin_x + (size_t)m * e.N + n0) = pk;
       }
     };
+    // the residual entering the finalisation: fin_resid (+ the fixed-point accumulator, whose entries this tile's
+    // finalising workgroup then clears: every split of the tile loaded them before its ticket)
+    auto fin_base = [&](int t) {
+      f32x4 b = fin_r[t];
+      if (f.fx) b += f32x4{fx_to_f32(fin_fa[t][0]), fx_to_f32(fin_fa[t][1]), fx_to_f32(fin_fb[t][0]),
+                           fx_to_f32(fin_fb[t][1])};
+      return b;
+    };
+    auto fx_clear = [&](int n0) {
+      if (f.fx) {
+        long long* p = f.fx + (size_t)m * e.N + n0;
+        *(i64x2*)p = i64x2{0, 0};
+        *(i64x2*)(p + 2) = i64x2{0, 0};
+      }
+    };
     auto put_ss = [&](float (&ssl)[SE]) {
 #pragma unroll
       for (int p = 0; p < SE; ++p) {
@@ -1330,7 +1378,8 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
         if (m < M && n0 < e.N) {
           f32x4 v = acc[t];
           if (e.bias) v += load4_guard(e.bias, n0, e.N);
-          finish(t, n0, fin_r[t] + v, ssl[t / 2 < SE ? t / 2 : 0]);
+          finish(t, n0, fin_base(t) + v, ssl[t / 2 < SE ? t / 2 : 0]);
+          fx_clear(n0);
         }
       }
       put_ss(ssl);
@@ -1362,7 +1411,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     for (int t = 0; t < NT; ++t) {
       const int n0 = (tile0 + t) * 16 + q;
       if (m < M && n0 < e.N) {
-        f32x4 v = fin_r[t];
+        f32x4 v = fin_base(t);
         // all (<= 8) slabs in flight at once: clamped addresses + selects, no per-split branch / wait
         const int Z = gi.ny;
         u32x2 sa[8], sb[8];
@@ -1379,6 +1428,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
           v += zz < Z ? sv : f32x4{0.f, 0.f, 0.f, 0.f};
         }
         finish(t, n0, v, ssl[t / 2 < SE ? t / 2 : 0]);
+        fx_clear(n0);
       }
     }
     put_ss(ssl);
@@ -1399,6 +1449,25 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
           float* dst = (float*)e.C + (size_t)m * e.ldc + n0;
 #pragma unroll
           for (int j = 0; j < 4; ++j) unsafeAtomicAdd(dst + j, v[j]);
+        }
+      }
+    }
+    return;
+  }
+  if constexpr (EPI == PG_EPI_FX_ADD) {
+    // C[m][n] += rn(acc * 2^32) by 64-bit integer atomics (global_atomic_add_u64 at the memory side): the same one
+    // round trip after the last MFMA as F32_ADD, but integer addition is associative, so the accumulated sum --
+    // and every residual read from it -- is the same bits whatever order the splits arrive in
+    if (m < M) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int n0 = (tile0 + t) * 16 + q;
+        if (n0 < e.N) {
+          f32x4 v = acc[t];
+          if (e.bias && z == 0) v += load4_guard(e.bias, n0, e.N);
+          unsigned long long* dst = (unsigned long long*)e.C + (size_t)m * e.ldc + n0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) atomicAdd(dst + j, (unsigned long long)fx_from_f32(v[j]));
         }
       }
     }
@@ -1598,7 +1667,9 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(xs8 + pi * 1024), 16, 0, 0);
     }
   }
-  const int my_pieces = (MT * 16 * Kr / 1024 - wave + 3) / 4;   // this wave's DMA pieces (vmcnt bookkeeping)
+  // the x DMA pieces stay ahead of every W load in the vmcnt order (step 3 waits for "at most the W loads
+  // outstanding"): the scheduler may not hoist a W load above them
+  __builtin_amdgcn_sched_barrier(0);
   const uint8_t* wt[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t) wt[t] = W + (size_t)min(tile0 + t, (e.N >> 4) - 1) * 16 * K + lane * 16;
@@ -1623,7 +1694,6 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
   // 3. this wave's x pieces have landed once at most its W loads are outstanding; the barrier covers the others'
   {
     const int wl = (CPW > 0 ? min(DEPTH, CPW) : min(DEPTH, nch)) * NTW * 2;
-    (void)my_pieces;
     wait_vm_n(wl);
     if constexpr (XB) {
 #pragma unroll
@@ -2032,7 +2102,7 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
 template <int EPI, bool FRAG>
 static void launch_gemv(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K, int ksplit, const EpiArgs& e,
                         hipStream_t st) {
-  if constexpr (EPI == PG_EPI_F32_ADD) {     // (plain x, or the attention merge: o_proj / down_proj)
+  if constexpr (EPI == PG_EPI_F32_ADD || EPI == PG_EPI_FX_ADD) {   // (plain x, or the attention merge: o / down)
     if (e.f.pro_mode == 2)
       launch_gemv_pro<EPI, 2, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
     else
@@ -2054,7 +2124,7 @@ static void launch_any(const bf16_t* A, int lda, const bf16_t* W, int ldw, int K
                        hipStream_t st, bool m1 = false, bool n64 = false) {
   if (e.M <= 16)
     launch_gemv<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st);
-  else if constexpr (EPI != PG_EPI_F32_FIN && EPI != PG_EPI_F32_ADD)
+  else if constexpr (EPI != PG_EPI_F32_FIN && EPI != PG_EPI_F32_ADD && EPI != PG_EPI_FX_ADD)
     launch_tile<EPI, FRAG>(A, lda, W, ldw, K, ksplit, e, st, m1, n64);
 }
 
@@ -2073,7 +2143,8 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag && !fp8) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
                        (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||
-                        epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD));
+                        epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD ||
+                        epi == PG_EPI_FX_ADD));
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
@@ -2104,7 +2175,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                         ldc == N);
   if (epi == PG_EPI_F32_ADD) PG_REQUIRE((M <= 16 || (fp8 && frag && M <= 32)) && (f.pro_mode == 0 || f.pro_mode == 2) &&
                                         ldc >= N);
-  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD);
+  if (epi == PG_EPI_FX_ADD) PG_REQUIRE(M <= 16 && !fp8 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N &&
+                                       ((uintptr_t)C & 15) == 0 && ldc % 2 == 0);
+  if (f.fx) PG_REQUIRE(((uintptr_t)f.fx & 15) == 0 && (f.pro_mode == 1) != (epi == PG_EPI_F32_FIN) && !fp8 &&
+                       M <= 16);
+  if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD || epi == PG_EPI_FX_ADD);
   if (epi == PG_EPI_BF16_GELU_MUL) PG_REQUIRE(N % 32 == 0);
   if (epi == PG_EPI_F32_POS) PG_REQUIRE(aux != nullptr && aux_rows > 0 && bias != nullptr);
   if (epi == PG_EPI_BF16_VT) PG_REQUIRE(aux_out != nullptr && aux_n % 4 == 0);
@@ -2162,6 +2237,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
     PG_CASE(PG_EPI_QKV_ROPE)
     PG_CASE(PG_EPI_F32_FIN)
     PG_CASE(PG_EPI_F32_ADD)
+    PG_CASE(PG_EPI_FX_ADD)
     PG_CASE_ROWMAJOR(PG_EPI_BF16_GELU)
     PG_CASE_ROWMAJOR(PG_EPI_F32_POS)
     PG_CASE_ROWMAJOR(PG_EPI_BF16_VT)

@@ -143,10 +143,13 @@ class PaliGemmaEngine:
     # pg_quant_fp8 launch; same bytes)
     ATTN_FP8_OUT = os.environ.get("PG_ATTN_FP8_OUT", "1") != "0"
     # B <= FUSE_MAX_B single rank: row-parallel decode linears that add their split-K partials straight into the
-    # residual with float atomics (PG_EPI_F32_ADD) instead of finalising slabs in-kernel (F32_FIN's slab store ->
-    # ticket -> slab load tail); the next GEMV then normalises the residual itself (PRO_RMSNORM).  "down": down_proj
-    # of every layer but the last (whose FIN output feeds the lm_head); "both": o_proj too; "0": off
-    DECODE_ADD = os.environ.get("PG_DECODE_ADD", "both")
+    # residual instead of finalising slabs in-kernel (F32_FIN's slab store -> ticket -> slab load tail); the next GEMV
+    # then normalises the residual itself (PRO_RMSNORM).  "fx" (default): o_proj and down_proj add into a fixed-point
+    # int64 accumulator with integer atomics (PG_EPI_FX_ADD) -- the sum is exact, so decode is bit-reproducible run to
+    # run; "both": the same with float atomics into the fp32 residual (unordered: ~1 ulp run-to-run drift); "down":
+    # down_proj only, float atomics; "0": off (F32_FIN, deterministic).  The last layer's down_proj always finalises
+    # (F32_FIN), its x' and sums of squares feeding the lm_head
+    DECODE_ADD = os.environ.get("PG_DECODE_ADD", "fx")
     # fp8 linears of 17..32 rows (batched decode, the lm_head of a 17..32-row batch) on the weight-streaming fp8 GEMV
     # (fragment-packed e4m3 weights, csrc/gemm.hip gemv8_kernel) instead of the LDS-staged fp8 tile GEMM
     FP8_GEMV = os.environ.get("PG_FP8_GEMV", "1") != "0"
@@ -495,7 +498,9 @@ class PaliGemmaEngine:
         if self.tp == 1:
             self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
             return ks
-        C = T // self.AR_CHUNK_ROWS if T >= 2 * self.AR_CHUNK_ROWS else 1
+        # at most AR_CHUNK_ROWS rows per chunk (4096 x 2048 fp32 = the xGMI exchange's 2^23 cap: no chunk spills to
+        # the process group)
+        C = -(-T // self.AR_CHUNK_ROWS) if T >= 2 * self.AR_CHUNK_ROWS else 1
         if C <= 1:
             self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
             return self.comm.all_reduce_slabs(part[:ks], ks)
@@ -723,15 +728,18 @@ class PaliGemmaEngine:
         xq = self._buf("d_xq", (B, H), torch.bfloat16)
         SK = SK or self.DECODE_SPLIT_KEYS
         nl = len(w.tl)
-        add_down = merge_in_gemv and self.DECODE_ADD in ("down", "both")
-        add_o = merge_in_gemv and self.DECODE_ADD == "both"
+        add_down = merge_in_gemv and self.DECODE_ADD in ("down", "both", "fx")
+        add_o = merge_in_gemv and self.DECODE_ADD in ("both", "fx")
+        # "fx": the partials go to the fixed-point accumulator (zero between steps: the last layer's F32_FIN clears it)
+        fx = self._zeros("d_fx", (B, H), torch.int64) if merge_in_gemv and self.DECODE_ADD == "fx" else None
+        add_epi, add_dst = (ops.EPI_FX_ADD, fx) if fx is not None else (ops.EPI_F32_ADD, res)
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                         q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
             if i == 0 or add_down:  # the residual rows are final (embedding, or atomically added): RMSNorm prologue
-                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["in_w"], eps=1e-6,
-                                    **rope)
+                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, fx=fx, nsplit=0, norm_w=Lw["in_w"],
+                                    eps=1e-6, **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
@@ -746,7 +754,7 @@ class PaliGemmaEngine:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                         head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
                                         akeys=SK)
-                    ops.gemm_fused(None, Lw["o_w"], res, fa, epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=so)
+                    ops.gemm_fused(None, Lw["o_w"], add_dst, fa, epi=add_epi | w.wflag, M=B, ksplit=so)
                 else:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                         head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
@@ -760,24 +768,29 @@ class PaliGemmaEngine:
                 ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
             self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd,
-                          add=add_down and i + 1 < nl, gu_rms=add_o)
+                          add=add_down and i + 1 < nl, gu_rms=add_o, fx=fx)
         return xq, ss_d, tiles, n_ss
 
-    def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd, add=False, gu_rms=False):
+    def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd, add=False, gu_rms=False,
+                 fx=None):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
         (x' of the next norm -> xq, its sums of squares -> ss_d).  add: down adds its partials into res with float
-        atomics (EPI_F32_ADD; the next GEMV normalises res itself).  gu_rms: o_proj did so, gate/up normalises res."""
+        atomics (EPI_F32_ADD), or into the fixed-point accumulator fx (EPI_FX_ADD); the next GEMV normalises res (+ fx)
+        itself.  gu_rms: o_proj did so, gate/up normalises res (+ fx).  The finalising form adds fx and clears it."""
         w = self.w
         if gu_rms:
-            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, nsplit=0, norm_w=Lw["post_w"], eps=1e-6)
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, fx=fx, nsplit=0, norm_w=Lw["post_w"], eps=1e-6)
             ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
         else:
             fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)
             ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
         if add:
-            ops.gemm_fused(h, Lw["down_w"], res, ops.fused_args(), epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=sd)
+            if fx is not None:
+                ops.gemm_fused(h, Lw["down_w"], fx, ops.fused_args(), epi=ops.EPI_FX_ADD | w.wflag, M=B, ksplit=sd)
+            else:
+                ops.gemm_fused(h, Lw["down_w"], res, ops.fused_args(), epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=sd)
             return
-        fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w)
+        fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss_d, ss_ld=tiles, fin_x=xq, norm_w=nxt_w, fx=fx)
         ops.gemm_fused(h, Lw["down_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=sd)
 
     def _split_keys(self, B: int, Smax: int) -> int:

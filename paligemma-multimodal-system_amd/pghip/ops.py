@@ -15,7 +15,8 @@ import torch
 from . import _lib
 
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN, \
-    EPI_F32_ADD = range(9)
+    EPI_F32_ADD, EPI_FX_ADD = range(10)
+FX_SCALE = 2.0 ** 32   # PG_EPI_FX_ADD: the int64 accumulator holds round(value * 2^32)
 PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
 NORM_LAYER, NORM_RMS = 0, 1
 W_FRAG = 0x100   # OR into epi: W is fragment-packed (weights.frag_pack, include/pghip.h PG_W_FRAG)
@@ -176,6 +177,8 @@ def gemm_fused(A: Optional[torch.Tensor], W: torch.Tensor, out: torch.Tensor, fa
     `fa` is a PgFusedArgs (see fused_args); `keep` holds tensors it points to alive for the call."""
     _chk(W, torch.bfloat16, "W")
     _chk_frag(W, epi)
+    if (epi & 0xFF) == EPI_FX_ADD:
+        _chk(out, torch.int64, "out (the fixed-point accumulator)")
     N = W.shape[0] if N is None else N
     K = W.shape[1]
     if ldc is None:

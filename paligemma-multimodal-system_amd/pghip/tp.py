@@ -116,6 +116,7 @@ class XgmiComm(TPComm):
         self.epochs = torch.zeros(64, dtype=torch.int32, device="cuda")
         self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
         self._side = None
+        self.fallbacks = 0                            # collectives carried by the process group instead (too large)
         self._dist.barrier(group=self.group)          # every rank mapped every buffer before first use
         self.capturable = True
 
@@ -138,6 +139,7 @@ class XgmiComm(TPComm):
                            torch.cuda.current_stream().cuda_stream)
         else:
             self._refuse_in_capture("all-reduce", t)
+            self.fallbacks += 1
             super().all_reduce(t)
 
     def all_reduce_slabs(self, part: torch.Tensor, ns: int) -> int:
@@ -153,6 +155,8 @@ class XgmiComm(TPComm):
 
     def all_reduce_async(self, t: torch.Tensor):
         if not self._ok(t):
+            if self.backend != "gloo":                # (gloo runs it through self.all_reduce, which counts it)
+                self.fallbacks += 1
             return super().all_reduce_async(t)
         # the exchange on a side stream that first waits for everything enqueued so far on the current one
         if self._side is None:
@@ -166,12 +170,30 @@ class XgmiComm(TPComm):
 
     def all_gather(self, out: torch.Tensor, t: torch.Tensor):
         t = t.contiguous()
-        if self._ok(t) and out.is_contiguous() and out.numel() == self.world * t.numel() and out.data_ptr() % 16 == 0:
-            self._lib.call("pg_allgather_xgmi", t.data_ptr(), t.numel(), out.data_ptr(), self.rank, self.world,
+        n = t.numel()
+        if self._ok(t) and out.is_contiguous() and out.numel() == self.world * n and out.data_ptr() % 16 == 0:
+            self._lib.call("pg_allgather_xgmi", t.data_ptr(), n, out.data_ptr(), self.rank, self.world,
                            self._peers, self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
                            torch.cuda.current_stream().cuda_stream)
+        elif (t.is_cuda and t.dtype == torch.float32 and n > self.cap and n % 4 == 0 and out.is_contiguous()
+              and out.numel() == self.world * n and t.data_ptr() % 16 == 0 and not torch.cuda.is_current_stream_capturing()):
+            # larger than the exchange (the SigLIP features of several images per rank): pieces of at most `cap`
+            # elements, each gathered into a [world][piece] staging tensor and copied to its rank-strided place
+            piece = self.cap
+            stage = torch.empty(self.world, piece, dtype=torch.float32, device=t.device)
+            ov = out.view(self.world, n)
+            for k0 in range(0, n, piece):
+                k1 = min(n, k0 + piece)
+                st = stage[:, : k1 - k0]
+                if k1 - k0 < piece:
+                    st = stage.view(-1)[: self.world * (k1 - k0)].view(self.world, k1 - k0)
+                self._lib.call("pg_allgather_xgmi", t.data_ptr() + 4 * k0, k1 - k0, st.data_ptr(), self.rank,
+                               self.world, self._peers, self.cap, self.epochs.data_ptr(), self.err.data_ptr(),
+                               torch.cuda.current_stream().cuda_stream)
+                ov[:, k0:k1].copy_(st)
         else:
             self._refuse_in_capture("all-gather", t)
+            self.fallbacks += 1
             super().all_gather(out, t)
 
     def check(self):

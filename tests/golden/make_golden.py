@@ -16,6 +16,7 @@ with the reference's own ``load_state_dict(strict=False)`` + ``tie_weights``
 (utils.py:33-36).
 
 Usage:  python tests/golden/make_golden.py [tiny] [tiny8] [pt224] [pt448wc] [pt896wc] [topp] [pt448] [pt896] [pt224wc]
+        [processor] [main]
 """
 from __future__ import annotations
 
@@ -391,6 +392,52 @@ def make_topp(inference):
     print("topp: kept sizes", [len(cases[f"c{i}_kept_ids"]) for i in range(4)])
 
 
+def make_main(mp, inference):
+    """BASELINE configs[0] end to end: the reference's own inference.main (inference.py:109-150: load_hf_model ->
+    PaliGemmaProcessor -> test_inference, CPU, greedy) on the model directory and RGBA image of tests/main_fixture.py.
+    Stores what it prints (the prompt + decoded line), the generated ids (captured at the tokenizer's decode) and each
+    step's top1-top2 logit margin (captured at the model's forward)."""
+    import shutil
+    import main_fixture as MF
+    from transformers import PreTrainedTokenizerBase
+    d = tempfile.mkdtemp()
+    try:
+        cfg = MF.write_model_dir(os.path.join(d, "model"))
+        img = MF.write_image(os.path.join(d, "pic.png"))
+        decoded_ids, margins = [], []
+        real_decode = PreTrainedTokenizerBase.decode
+
+        def decode(self, token_ids, *a, **k):
+            decoded_ids.append([int(t) for t in token_ids])
+            texts.append(real_decode(self, token_ids, *a, **k))
+            return texts[-1]
+        texts = []
+        real_fwd = mp.PaliGemmaForConditionalGeneration.forward
+
+        def fwd(self, *a, **k):
+            out = real_fwd(self, *a, **k)
+            top = torch.topk(out["logits"][0, -1].float(), 2).values
+            margins.append(float(top[0] - top[1]))
+            return out
+        PreTrainedTokenizerBase.decode, mp.PaliGemmaForConditionalGeneration.forward = decode, fwd
+        buf = io.StringIO()
+        try:
+            with contextlib.redirect_stdout(buf):
+                inference.main(model_path=os.path.join(d, "model"), prompt=MF.PROMPT, image_file_path=img,
+                               max_tokens_to_generate=MF.MAX_TOKENS, do_sample=False, only_cpu=True)
+        finally:
+            PreTrainedTokenizerBase.decode, mp.PaliGemmaForConditionalGeneration.forward = real_decode, real_fwd
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    printed = MF.PROMPT + texts[-1]                              # inference.py:87 prints prompt + decoded
+    assert printed in buf.getvalue()
+    out = {"stdout": np.array(buf.getvalue()), "printed": np.array(printed),
+           "ids": np.array(decoded_ids[-1], dtype=np.int64), "margins": np.array(margins, dtype=np.float32),
+           "vocab_size": np.int64(cfg["text_config"]["vocab_size"]), "image_token_index": np.int64(cfg["image_token_index"])}
+    np.savez_compressed(os.path.join(HERE, "main.npz"), **out)
+    print("main:", repr(printed), "| ids", out["ids"].tolist(), "| min margin", float(out["margins"].min()))
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["tiny", "topp", "pt224", "pt448", "pt896"]
     mp, inference, proc = import_reference()
@@ -418,3 +465,6 @@ if __name__ == "__main__":
     if "pt896wc" in which:
         make_large(mp, inference, proc, "pt896wc", configs.PT_896, [1234, 1235], steps=16, row_stride=256,
                    linear_gain=1.6, memo=True)
+    if "main" in which:           # BASELINE configs[0]: the reference's inference.main end to end
+        sys.path.insert(0, os.path.dirname(HERE))
+        make_main(mp, inference)

@@ -209,6 +209,46 @@ def test_pt224_full_size_teacher_forced_decode(golden):
     assert checked == int((g["margin"] > 0.5).sum()) == 4, checked
 
 
+@pytest.mark.slow
+def test_pt224_decode_bit_reproducible_run_to_run(golden):
+    """The same full-size PaliGemma-3B-224 request decoded three times in one process -- eager steps, hipGraph
+    replays, eager again -- gives bitwise-equal logits at every step and the same ids (greedy ids
+    must not depend on the run).  Batch-1 decode adds the o_proj / down_proj split-K partials into the residual with
+    atomics whose arrival order varies; the default fixed-point accumulator (PG_EPI_FX_ADD, engine.DECODE_ADD "fx")
+    makes that sum exact, so nothing downstream can differ.  The prefill logits are compared too."""
+    from pghip import configs, engine, synthetic, weights
+    g = golden("pt224")
+    cfg = configs.PT_224
+    eng = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, synthetic.SyntheticStateDict(cfg).__getitem__))
+    assert eng.DECODE_ADD == "fx"
+    ids = torch.from_numpy(g["input_ids"]).cuda()
+    px = torch.from_numpy(g["pixel_values"]).cuda()
+    steps, V = 24, eng.w.vocab
+
+    def run(graph):
+        cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), steps + 1)
+        sampler = dict(do_sample=False)
+        st = eng.decode_state(1, cache, nxt, steps + 1, sampler=sampler)
+        eng.sample(logits, st, sampler, advance=False, feats=feats)
+        out = [logits[:, :V].clone()]
+        replay = eng._graph_step(st, cache, feats, sampler) if graph else None
+        for _ in range(steps):
+            if graph:
+                replay()
+                lg = eng._buf("d_logits", (1, eng.w.vocab_local_pad), torch.float32)[:, :V]
+            else:
+                lg = eng.decode_step(st, cache, feats, sampler)
+            out.append(lg.clone())
+        torch.cuda.synchronize()
+        return torch.cat(out), st["hist"][:steps + 1, 0].cpu()
+
+    runs = [run(False), run(True), run(False)]
+    for lg, hist in runs[1:]:
+        assert torch.equal(hist, runs[0][1]), (hist.tolist(), runs[0][1].tolist())
+        diff = (lg != runs[0][0]).any(-1).nonzero().flatten().tolist()
+        assert not diff, f"logits differ at steps {diff}"
+
+
 def test_batched_generation_per_row_eos(tiny, golden):
     """B = 2 rows of the same request (+ one different image): each row equals its own B = 1 run, cut at
     its own EOS (tokens after a row's EOS come back as pad)."""

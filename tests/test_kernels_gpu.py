@@ -892,11 +892,16 @@ def test_norm_residual_fp8_equals_quantised_bf16_output(M, H, nsplit):
 
 
 @pytest.mark.parametrize("M,N,K,ks", [(32, 2560, 2048, 1), (17, 2048, 16384, 8), (24, 4096, 2048, 2),
-                                      (9, 512, 256, 1), (32, 32160, 2048, 1), (32, 16384, 2048, 1)])
+                                      (9, 512, 256, 1), (32, 32160, 2048, 1), (32, 16384, 2048, 1),
+                                      # ragged K splits (the runtime-trip-count forms, CPW = 0): K-split and wide
+                                      # kernels; and more splits than 128-k chunks (the last splits own none)
+                                      (20, 1024, 1152, 2), (32, 4096, 2048, 3), (20, 16384, 1152, 2),
+                                      (24, 512, 256, 4), (24, 16384, 256, 4)])
 def test_gemv8_fragment_packed_matches_the_fp8_tile_gemm(M, N, K, ks):
     """The fp8 weight-streaming GEMV (fragment-packed e4m3 weights, weights.frag_pack8; 17..32-row batched decode and
     the fp8 lm_head): equal to a torch fp32 matmul of the dequantised operands up to fp32 summation order, for the
-    fp32 slab (split-K), bf16 and gelu*up epilogues; the pack / unpack pair is a bijection."""
+    fp32 slab (split-K), bf16 and gelu*up epilogues; the pack / unpack pair is a bijection.  Splits past the last
+    128-k chunk write zero slabs."""
     from pghip import ops
     from pghip.weights import frag_pack8, frag_unpack8, quant_rows_fp8
     A, W = rnd(M, K, seed=71), rnd(N, K, scale=1 / math.sqrt(K), seed=72)
@@ -993,3 +998,78 @@ def test_gemv_fin_residual_xprime_and_pair_sums(M, N, K, ks):
     pairs = (ref * ref).view(M, tiles // 2, 32).sum(-1)
     assert torch.allclose(ss[:, :tiles // 2], pairs, rtol=1e-4, atol=1e-3)
     assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("M,z,pro", [(1, 1, 0), (1, 8, 0), (2, 2, 0), (1, 2, 2), (2, 4, 2), (16, 3, 0)])
+def test_gemv_fx_add_fixed_point_residual(M, z, pro):
+    """PG_EPI_FX_ADD (ABI 10): the GEMV adds round(partial * 2^32) into an int64 accumulator with integer atomics.
+    The accumulated value equals x.W^T (+ bias once) to the fp32 reference's tolerance, rows past M stay zero, and --
+    the point of the fixed-point form -- the same launches give the same bits every time (integer addition is
+    associative, so the split arrival order does not matter); with the attention-merge prologue (o_proj) too."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    N = 1024
+    bias = torch.randn(N).cuda() * 0.1
+    if pro == 2:                    # o_proj: x is the merge of split-KV attention partials
+        nh, hd, nsplit, dt = 8, 256, 8, 256
+        K = nh * hd
+        po = torch.randn(M * nsplit * 16 * dt, device="cuda")
+        pml = torch.stack([torch.randn(M * nsplit * 16, device="cuda"),
+                           torch.rand(M * nsplit * 16, device="cuda") + 0.5], -1).reshape(-1).contiguous()
+        fa = lambda: ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=po, part_ml=pml, asplit=nsplit,  # noqa
+                                    head_dim=hd, dtw=dt, q_per_kv=nh, kv_heads=1)
+        x = torch.empty(M, K, dtype=torch.bfloat16, device="cuda")
+        ops.attn_combine(po, pml, x, K, B=M, Hq=nh, Hkv=1, D=hd, nsplit=nsplit)
+        A = None
+    else:
+        K = 2048
+        x = rnd(M, K, seed=33)
+        fa, A = ops.fused_args, x
+    W = rnd(N, K, scale=1 / 45, seed=34)
+    Wk = frag_pack(W)
+    runs = []
+    for _ in range(3):
+        acc = torch.zeros(M + 1, N, dtype=torch.int64, device="cuda")
+        ops.gemm_fused(A, Wk, acc, fa(), epi=ops.EPI_FX_ADD | ops.W_FRAG, M=M, ksplit=z, bias=bias)
+        runs.append(acc)
+    torch.cuda.synchronize()
+    ref = x.float() @ W.float().t() + bias
+    got = runs[0][:M].double() / ops.FX_SCALE
+    assert err(got.float(), ref) < 1e-5
+    assert int(runs[0][M:].abs().sum()) == 0
+    assert all(torch.equal(runs[0], r) for r in runs[1:])
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_fx_accumulator_consumers_rmsnorm_and_fin_clear(M):
+    """The consumers of the fixed-point accumulator: a pro_mode 1 GEMV normalises resid + fx, and a PG_EPI_F32_FIN
+    GEMV finalises resid + fx + its split-K slabs and leaves fx zero (the decode step's last down_proj)."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    H, N2, K2, ks = 2048, 2048, 4096, 4
+    resid = torch.randn(M, H).cuda()
+    delta = torch.randn(M, H).cuda()
+    fx = (delta.double() * ops.FX_SCALE).round().to(torch.int64)
+    dval = (fx.double() / ops.FX_SCALE).float()
+    w = torch.randn(H).cuda() * 0.1
+    W = rnd(512, H, scale=1 / 45, seed=35)
+    out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
+    fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=resid, fx=fx, nsplit=0, norm_w=w, eps=1e-6)
+    ops.gemm_fused(None, frag_pack(W), out, fa, epi=ops.EPI_BF16 | ops.W_FRAG, M=M)
+    xr = resid + dval
+    xn = (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)).to(torch.bfloat16).float()
+    assert err(out, xn @ W.float().t()) < 1e-2
+    # FIN: resid + fx + x.W^T, fx cleared
+    tiles = N2 // 16
+    x2, W2 = rnd(M, K2, seed=36), rnd(N2, K2, scale=1 / 64, seed=37)
+    res = resid.clone()
+    cnt = torch.zeros(tiles, dtype=torch.int32, device="cuda")
+    ss = torch.zeros(M, tiles, device="cuda")
+    xq = torch.empty(M, N2, dtype=torch.bfloat16, device="cuda")
+    part = torch.empty(ks, M, N2, device="cuda")
+    fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss, ss_ld=tiles, fin_x=xq, norm_w=w, fx=fx)
+    ops.gemm_fused(x2, frag_pack(W2), part, fa, epi=ops.EPI_F32_FIN | ops.W_FRAG, M=M, ksplit=ks)
+    torch.cuda.synchronize()
+    ref = resid + dval + x2.float() @ W2.float().t()
+    assert err(res, ref) < 1e-4
+    assert int(fx.abs().sum()) == 0 and int(cnt.abs().sum()) == 0

@@ -106,27 +106,51 @@ def test_tp_engine_on_one_device(tmp_path, cfg, world, comm, chunk, fp8):
     assert all(o["greedy"] == res[0]["greedy"] and o["sampled_tp"] == res[0]["sampled_tp"] for o in res)
 
 
-@pytest.mark.slow
-def test_tp8_pt896_fp8_batch8(tmp_path):
-    """BASELINE configs[4]'s model and split: PaliGemma-3B-pt-896 with fp8 Gemma linears at TP=8 (one q head, 2048
-    intermediate columns and 32,152 vocabulary rows per rank; modeling_gemma.py:205-218, 255-259, 356, 523), eight
-    ranks on one device, batch 8 (one image per rank through the data-parallel SigLIP).  Prefill (32,832 rows, the
-    all-reduces in 4096-row chunks) and 3 teacher-forced decode steps: row 0 against the reference's pt-896 request
-    (the fp8 bound of tests/test_large_gpu.py, 30% of the top-64 scale), every row against the single-rank fp8 engine
-    (the two quantise different weight slices: the same 30% bound, the same top-1 wherever the single-rank margin
-    exceeds 5% of the scale)."""
-    if not torch.cuda.is_available():
-        pytest.skip("needs the HIP device")
-    res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896")
+def _check_896(res, min_checked):
+    """Verdicts of tp_worker.full_size_896 (BASELINE configs[4]): bounded by the fp32 oracle run on the same e4m3 /
+    bf16 operand rounding (tests/golden/make_emu.py, <golden>_fp8emu.npz), not a flat percentage."""
     for o in res:
         assert o["xgmi_err"] == 0 and o["vision_dp"], o
-        assert o["ref_top64_err"] < 0.30, o
-        for t, (got, want, m, e) in enumerate(zip(o["ref_top1"], o["ref_ids"], o["ref_margin"], o["ref_top64_abs"])):
-            if m > 2 * e:                          # as test_large_gpu._check_step
-                assert got == want, (t, o)
+        assert o["fallbacks"] == 0, o                  # every collective went through the xGMI exchange
+        assert o["emu_ratio"] < 1.5, o                 # reference top-64 within 1.5x the emulated e4m3 distance
+        assert o["top1_bad"] == [] and o["top1_checked"] >= min_checked, o
+        assert o["row_spread"] < 2e-2, o               # rows of one request agree
     r0 = res[0]
-    assert r0["solo_ref_top64_err"] < 0.30 and r0["vs_solo_err"] < 0.30 and r0["vs_solo_top1_agree"], r0
-    assert all(o["ref_top1"] == r0["ref_top1"] for o in res)
+    assert r0["solo_emu_ratio"] < 1.5 and r0["solo_top1_bad"] == [], r0
+    assert r0["vs_solo_emu_ratio"] < 3.0 and r0["vs_solo_top1_agree"], r0
+    assert all(o["top1"] == r0["top1"] for o in res)
+
+
+@pytest.mark.slow
+def test_tp8_pt896_fp8_batch32(tmp_path):
+    """BASELINE configs[4] at its own shape: PaliGemma-3B-pt-896, batch 32, fp8 Gemma linears, TP=8 (one q head, 2048
+    gate/up columns, a 2048-row down slice and 32,152 vocabulary rows per rank; modeling_gemma.py:205-218, 255-259,
+    356, 523), eight ranks on one device over the xGMI exchange with cap 2^23 (every 4096-row prefill chunk and every
+    decode message fits: no collective travels over the process group).  The better-conditioned recipe's two images,
+    16 rows each (4 images per rank through the data-parallel SigLIP), prefill plus 15 teacher-forced decode steps on
+    the sharded 17..32-row fp8 GEMVs and the fp8 vocabulary-slice lm_head: every kept row within 1.5x the emulated e4m3
+    distance of the reference's top-64 logits, the reference's top-1 wherever its margin exceeds twice the step's
+    distance, and against the single-rank fp8 engine."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896", TP_B="32",
+                  TP_GOLDEN="pt896wc")
+    print(json.dumps({k: v for k, v in res[0].items() if k != "top1"}))
+    assert all(o["B"] == 32 and o["cap"] == 1 << 23 for o in res)
+    _check_896(res, min_checked=40)
+
+
+@pytest.mark.slow
+def test_tp8_pt896_fp8_batch8(tmp_path):
+    """The default recipe's pt-896 request (tests/golden/pt896.npz, 3 steps) at TP=8, batch 8 (one image per rank):
+    the same emulation-derived bounds as the batch-32 test.  Its top1-top2 margins (0.03-0.20) lie below the e4m3
+    error, so few steps reach the top-1 check."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896", TP_B="8",
+                  TP_GOLDEN="pt896")
+    print(json.dumps({k: v for k, v in res[0].items() if k != "top1"}))
+    _check_896(res, min_checked=0)
 
 
 @pytest.mark.slow

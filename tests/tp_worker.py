@@ -2,8 +2,8 @@
 transport, or pg_allreduce_xgmi with TP_COMM=xgmi): the tensor-parallel engine against the reference's golden vectors
 and the single-rank engine.  TP_CFG=tiny (default) / tiny8 use the tiny fixtures (tiny8: the 8-head toy for TP up to
 8); TP_CFG=pt-224 runs the full-size PaliGemma-3B-224 (BASELINE configs[3]'s mix-224 architecture) against
-tests/golden/pt224wc.npz; TP_CFG=pt-896 runs BASELINE configs[4]'s model (pt-896, fp8 Gemma linears) at batch 8
-against the single-rank engine and tests/golden/pt896.npz.  Writes one JSON verdict per rank to
+tests/golden/pt224wc.npz; TP_CFG=pt-896 runs BASELINE configs[4] (pt-896, fp8 Gemma linears, batch TP_B = 32) against
+the single-rank engine, tests/golden/pt896wc.npz and its fp8 emulation (or TP_GOLDEN=pt896: the default recipe).  Writes one JSON verdict per rank to
 $TP_OUT/rank<r>.json."""
 import json
 import os
@@ -273,72 +273,117 @@ def full_size(rank, world, name):
 
 
 def full_size_896(rank, world):
-    """BASELINE configs[4]'s model at TP = world: PaliGemma-3B-pt-896 (4096 image tokens), fp8 e4m3 Gemma linears,
-    batch 8 = one image per rank at TP=8 through the data-parallel SigLIP tower (its projected features all-gathered
-    in image order).  Row 0 is the reference's pt-896 request (tests/golden/pt896.npz), rows 1-7 other images.  The
-    32,832-row prefill cuts every o_proj / down_proj into 4096-row chunks whose all-reduces overlap the next chunk's
-    GEMM (engine._row_parallel; 33.5 MB chunks exceed the xGMI exchange here, so they travel over the process group),
-    then 3 teacher-forced decode steps (the reference's greedy ids; decode all-reduces over the xGMI exchange, graph
-    capturable).  Rank 0 then runs the same requests on the single-rank fp8 engine."""
+    """BASELINE configs[4] at its own shape: PaliGemma-3B-pt-896 (4096 image tokens), fp8 e4m3 Gemma linears, TP = world
+    (8: one q head, 2048 gate/up columns, a 2048-row down slice and 32,152 vocabulary rows per rank), TP_B rows (32 by
+    default: 4 images per rank through the data-parallel SigLIP, features all-gathered in image order) dealt in equal
+    blocks to the golden's images -- TP_GOLDEN pt896wc (default: the better-conditioned recipe's two requests, 16 rows
+    each, 16 steps) or pt896 (the default recipe's request, 3 steps).  The 131,328-row prefill cuts every o_proj /
+    down_proj into 4096-row chunks whose all-reduces (2^23 fp32 each) go through the xGMI exchange (cap 2^23: nothing
+    travels over the process group -- `fallbacks` counts what did), overlapping the next chunk's GEMM; then every
+    teacher-forced decode step on the 17..32-row fp8 GEMVs and the fp8 vocabulary-slice lm_head.  Rank 0 then runs the
+    same requests on the single-rank fp8 engine.  Writes, per (image, step, first/last row of the block), the top-64
+    distance to the reference's logits, the fp8 emulation's distance (<golden>_fp8emu.npz) and the top-1 check."""
     from PIL import Image
     from pghip import configs, engine, synthetic, weights
     from pghip.tp import TPComm, XgmiComm
     from processing_paligemma import process_images
     cfg = configs.PT_896
-    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "pt896.npz")))
-    sd = synthetic.SyntheticStateDict(cfg)
-    comm = XgmiComm(cap=1 << 20) if os.environ.get("TP_COMM") == "xgmi" else TPComm()
+    name = os.environ.get("TP_GOLDEN", "pt896wc")
+    B = int(os.environ.get("TP_B", "32"))
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz")))
+    em = dict(np.load(os.path.join(ROOT, "tests", "golden", f"{name}_fp8emu.npz")))
+    gain = float(g["linear_gain"]) if "linear_gain" in g else 2.0
+    sd = synthetic.SyntheticStateDict(cfg, linear_gain=gain)
+    xgmi = os.environ.get("TP_COMM", "xgmi") == "xgmi"
+    comm = XgmiComm(cap=1 << 23) if xgmi else TPComm()
     tp = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, tp_rank=rank, tp_world=world,
                                                            fp8=True), comm=comm)
-    B = 8
-    seeds = [int(g["seeds"][0])] + [2001 + b for b in range(1, B)]
+    images = list(range(len(g["seeds"])))
+    per = B // len(images)
     pv = []
-    for sd_ in seeds:
-        img = np.random.default_rng(sd_).integers(0, 256, (1, 896, 896, 3), dtype=np.uint8)
-        pv.append(np.stack(process_images([Image.fromarray(img[0])], 896, 1 / 255.0, Image.Resampling.BICUBIC)))
-    pv = np.concatenate(pv).astype(np.float32)
-    assert np.array_equal(pv[0].reshape(-1)[::9973], g["i0_pixel_sample"])
-    ids = torch.from_numpy(np.concatenate([g["i0_input_ids"]] * B)).cuda()
-    px = torch.from_numpy(pv).cuda()
-    ref_ids = g["i0_greedy_ids"].tolist()
-    steps = len(ref_ids)
+    for j in images:
+        img = np.random.default_rng(int(g["seeds"][j])).integers(0, 256, (1, 896, 896, 3), dtype=np.uint8)
+        p_ = np.stack(process_images([Image.fromarray(img[0])], 896, 1 / 255.0, Image.Resampling.BICUBIC))
+        assert np.array_equal(p_.astype(np.float32).reshape(-1)[::9973], g[f"i{j}_pixel_sample"])
+        pv += [p_] * per
+    ids = torch.from_numpy(np.concatenate([g[f"i{j}_input_ids"] for j in images for _ in range(per)])).cuda()
+    px = torch.from_numpy(np.concatenate(pv).astype(np.float32)).cuda()
+    steps = len(g["i0_greedy_ids"])
+    keep = [r for k in range(len(images)) for r in (k * per, k * per + per - 1)]      # first / last row of each block
 
     def run(e):
         cache, feats, logits, nxt = e.prefill_request(ids, px, torch.ones_like(ids), steps + 2)
         st = e.decode_state(B, cache, nxt, steps + 2)
+        # the top-p sampler path: full (vocabulary-gathered) logits every step; the teacher-forced ids overwrite its draw
         samp = dict(do_sample=True, temperature=0.8, top_p=0.9, uniforms=torch.full((steps + 3, B), 0.5, device="cuda"))
-        out = [logits.float().cpu().numpy()]
+        out, spread = [logits[keep].float().cpu().numpy()], [block_spread(logits)]
         for t in range(1, steps):
-            st["ids"].fill_(ref_ids[t - 1])
+            for k, j in enumerate(images):
+                st["ids"][k * per:(k + 1) * per].fill_(int(g[f"i{j}_greedy_ids"][t - 1]))
             st["step"].zero_()
-            out.append(e.decode_step(st, cache, feats, samp).float().cpu().numpy())
+            lg = e.decode_step(st, cache, feats, samp)
+            out.append(lg[keep].float().cpu().numpy())
+            spread.append(block_spread(lg))
         torch.cuda.synchronize()
-        return np.stack(out)                                        # [steps][B][V]
-    lg_tp = run(tp)
-    res = {"rank": rank, "world": world, "comm": type(comm).__name__, "chunks": tp.AR_CHUNK_ROWS,
-           "vision_dp": B >= world and B % world == 0}
+        return np.stack(out), max(spread)                           # [steps][len(keep)][V]
+
+    def block_spread(lg):
+        """max over the blocks of the rows' scaled distance to the block's first row (rows of one request agree)."""
+        worst = 0.0
+        for k in range(len(images)):
+            rows = lg[k * per:(k + 1) * per].float()
+            worst = max(worst, float((rows - rows[0]).abs().max() / rows[0].abs().max().clamp_min(1e-30)))
+        return worst
+
+    lg_tp, spread = run(tp)
+    res = {"rank": rank, "world": world, "B": B, "golden": name, "comm": type(comm).__name__,
+           "chunk_rows": tp.AR_CHUNK_ROWS, "vision_dp": B >= world and B % world == 0, "row_spread": spread,
+           "fallbacks": getattr(comm, "fallbacks", -1), "cap": getattr(comm, "cap", 0)}
     torch.cuda.synchronize()
     res["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
 
-    def top64(lg, t, scaled=True):
-        top_ids, top_v = g["i0_step_top_ids"][t], g["i0_step_top_values"][t]
-        return float(np.abs(lg[top_ids] - top_v).max() / (np.abs(top_v).max() if scaled else 1.0))
-    res["ref_top64_err"] = max(top64(lg_tp[t, 0], t) for t in range(steps))
-    res["ref_top64_abs"] = [top64(lg_tp[t, 0], t, False) for t in range(steps)]
-    res["ref_top1"] = [int(lg_tp[t, 0].argmax()) for t in range(steps)]
-    res["ref_ids"] = ref_ids
-    res["ref_margin"] = [float(m) for m in g["i0_margin"]]
+    def checks(lg):
+        """Per (image, step, kept row): top-64 distance / the emulation's, and the top-1 checks where the reference's
+        margin exceeds twice the measured distance (test_large_gpu._check_step)."""
+        ratio, checked, bad = 0.0, 0, []
+        for k, j in enumerate(images):
+            p = f"i{j}_"
+            for t in range(steps):
+                top_ids, top_v = g[p + "step_top_ids"][t], g[p + "step_top_values"][t]
+                emu = float(np.abs(em[p + "emu_top_values"][t] - top_v).max())
+                for r in (2 * k, 2 * k + 1):
+                    e = float(np.abs(lg[t, r][top_ids] - top_v).max())
+                    ratio = max(ratio, e / emu)
+                    if g[p + "margin"][t] > 2 * e:
+                        checked += 1
+                        if int(lg[t, r].argmax()) != int(g[p + "greedy_ids"][t]):
+                            bad.append((j, t, r, int(lg[t, r].argmax()), int(g[p + "greedy_ids"][t])))
+        return ratio, checked, bad
+
+    res["emu_ratio"], res["top1_checked"], res["top1_bad"] = checks(lg_tp)
+    res["top1"] = [[int(lg_tp[t, r].argmax()) for r in range(len(keep))] for t in range(steps)]
     if rank == 0:
         del tp
         torch.cuda.empty_cache()
         solo = engine.PaliGemmaEngine(cfg, weights.PackedWeights(cfg, sd.__getitem__, fp8=True))
-        lg_solo = run(solo)
-        res["solo_ref_top64_err"] = max(top64(lg_solo[t, 0], t) for t in range(steps))
-        res["vs_solo_err"] = max(err(lg_tp[t], lg_solo[t]) for t in range(steps))
-        res["vs_solo_top1_agree"] = all(
-            int(lg_tp[t, b].argmax()) == int(lg_solo[t, b].argmax()) or
-            np.sort(lg_solo[t, b])[-1] - np.sort(lg_solo[t, b])[-2] < 0.05 * np.abs(lg_solo[t, b]).max()
-            for t in range(steps) for b in range(B))
+        lg_solo, _ = run(solo)
+        res["solo_emu_ratio"], res["solo_top1_checked"], res["solo_top1_bad"] = checks(lg_solo)
+        # TP and single rank quantise different weight slices (row-parallel K slices get their own scales): each lies
+        # within 1.5x the emulated e4m3 distance of the reference, so their mutual distance on the reference's top-64
+        # ids is bounded by 3x that distance; top-1 equal wherever the single-rank margin exceeds twice the distance
+        vs, agree = 0.0, True
+        for k, j in enumerate(images):
+            p = f"i{j}_"
+            for t in range(steps):
+                top_ids, top_v = g[p + "step_top_ids"][t], g[p + "step_top_values"][t]
+                emu = float(np.abs(em[p + "emu_top_values"][t] - top_v).max())
+                for r in (2 * k, 2 * k + 1):
+                    d = float(np.abs(lg_tp[t, r][top_ids] - lg_solo[t, r][top_ids]).max())
+                    vs = max(vs, d / emu)
+                    srt = np.sort(lg_solo[t, r])
+                    if srt[-1] - srt[-2] > 2 * float(np.abs(lg_tp[t, r] - lg_solo[t, r]).max()):
+                        agree &= int(lg_tp[t, r].argmax()) == int(lg_solo[t, r].argmax())
+        res["vs_solo_emu_ratio"], res["vs_solo_top1_agree"] = vs, bool(agree)
         del solo
     if isinstance(comm, XgmiComm):
         comm.close()
