@@ -105,9 +105,12 @@ typedef struct PgFusedArgs {
   int amax_zero_n;
   /* ABI 10: */
   int64_t* fx;              /* fixed-point residual accumulator [M][K] (value = q * 2^-32, |value| < 2^31) written by
-                               PG_EPI_FX_ADD producers.  pro_mode 1: x = RMSNorm(resid_in + fx + sum partials) ;
-                               PG_EPI_F32_FIN (pro_mode != 1): the finalised residual is fin_resid + fx + slabs, and
-                               the launch leaves fx zero (each tile's finalising workgroup clears its entries)       */
+                               PG_EPI_FX_ADD producers; a PG_EPI_FX_ADD launch with resid_in set also adds those fp32
+                               rows (split 0), after which fx holds the whole residual.  pro_mode 1: x =
+                               RMSNorm(resid_in (may be NULL) + fx + sum partials) ; PG_EPI_F32_FIN (pro_mode != 1):
+                               the finalised residual is fx + slabs (written to fin_resid, whose old rows are not
+                               read), and the launch leaves fx zero (each tile's finalising workgroup clears its
+                               entries)                                                                           */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,

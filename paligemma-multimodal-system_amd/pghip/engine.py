@@ -730,7 +730,8 @@ class PaliGemmaEngine:
         nl = len(w.tl)
         add_down = merge_in_gemv and self.DECODE_ADD in ("down", "both", "fx")
         add_o = merge_in_gemv and self.DECODE_ADD in ("both", "fx")
-        # "fx": the partials go to the fixed-point accumulator (zero between steps: the last layer's F32_FIN clears it)
+        # "fx": the partials go to the fixed-point accumulator (zero between steps: the last layer's F32_FIN clears it);
+        # layer 0's o_proj also folds the embedding rows in, so from there on it holds the whole residual
         fx = self._zeros("d_fx", (B, H), torch.int64) if merge_in_gemv and self.DECODE_ADD == "fx" else None
         add_epi, add_dst = (ops.EPI_FX_ADD, fx) if fx is not None else (ops.EPI_F32_ADD, res)
         for i, Lw in enumerate(w.tl):
@@ -738,8 +739,10 @@ class PaliGemmaEngine:
                         slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                         q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
             if i == 0 or add_down:  # the residual rows are final (embedding, or atomically added): RMSNorm prologue
-                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, fx=fx, nsplit=0, norm_w=Lw["in_w"],
-                                    eps=1e-6, **rope)
+                # (fx mode: layer 0 reads the embedding rows; from layer 0's o_proj on the accumulator holds the whole
+                # residual -- that launch folds res in -- and the consumers read it alone)
+                fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res if (i == 0 or fx is None) else None,
+                                    fx=fx if i > 0 else None, nsplit=0, norm_w=Lw["in_w"], eps=1e-6, **rope)
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
@@ -753,7 +756,7 @@ class PaliGemmaEngine:
                 if add_o:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                         head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
-                                        akeys=SK)
+                                        akeys=SK, resid_in=res if (fx is not None and i == 0) else None)
                     ops.gemm_fused(None, Lw["o_w"], add_dst, fa, epi=add_epi | w.wflag, M=B, ksplit=so)
                 else:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
@@ -779,7 +782,8 @@ class PaliGemmaEngine:
         itself.  gu_rms: o_proj did so, gate/up normalises res (+ fx).  The finalising form adds fx and clears it."""
         w = self.w
         if gu_rms:
-            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res, fx=fx, nsplit=0, norm_w=Lw["post_w"], eps=1e-6)
+            fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res if fx is None else None, fx=fx, nsplit=0,
+                                norm_w=Lw["post_w"], eps=1e-6)
             ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
         else:
             fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_o, ss_ld=tiles, ss_n=n_ss, eps=1e-6)

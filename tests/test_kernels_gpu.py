@@ -1042,27 +1042,32 @@ def test_gemv_fx_add_fixed_point_residual(M, z, pro):
 
 @pytest.mark.parametrize("M", [1, 2])
 def test_fx_accumulator_consumers_rmsnorm_and_fin_clear(M):
-    """The consumers of the fixed-point accumulator: a pro_mode 1 GEMV normalises resid + fx, and a PG_EPI_F32_FIN
-    GEMV finalises resid + fx + its split-K slabs and leaves fx zero (the decode step's last down_proj)."""
+    """The fixed-point accumulator's life in a decode step: an FX_ADD launch with resid_in folds the fp32 residual rows
+    into it (split 0) beside its own partials; a pro_mode 1 GEMV normalises the accumulator alone (resid_in null) or
+    resid_in + fx; a PG_EPI_F32_FIN GEMV finalises fx + its split-K slabs into fin_resid (not reading fin_resid's old
+    rows) and leaves fx zero (the step's last down_proj)."""
     from pghip import ops
     from pghip.weights import frag_pack
     H, N2, K2, ks = 2048, 2048, 4096, 4
     resid = torch.randn(M, H).cuda()
-    delta = torch.randn(M, H).cuda()
-    fx = (delta.double() * ops.FX_SCALE).round().to(torch.int64)
+    xo, Wo = rnd(M, 1024, seed=38), rnd(H, 1024, scale=1 / 32, seed=39)
+    fx = torch.zeros(M, H, dtype=torch.int64, device="cuda")
+    ops.gemm_fused(xo, frag_pack(Wo), fx, ops.fused_args(resid_in=resid), epi=ops.EPI_FX_ADD | ops.W_FRAG, M=M, ksplit=2)
+    torch.cuda.synchronize()
     dval = (fx.double() / ops.FX_SCALE).float()
+    assert err(dval, resid + xo.float() @ Wo.float().t()) < 1e-5
     w = torch.randn(H).cuda() * 0.1
     W = rnd(512, H, scale=1 / 45, seed=35)
-    out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
-    fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=resid, fx=fx, nsplit=0, norm_w=w, eps=1e-6)
-    ops.gemm_fused(None, frag_pack(W), out, fa, epi=ops.EPI_BF16 | ops.W_FRAG, M=M)
-    xr = resid + dval
-    xn = (xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)).to(torch.bfloat16).float()
-    assert err(out, xn @ W.float().t()) < 1e-2
-    # FIN: resid + fx + x.W^T, fx cleared
+    xn = (dval * torch.rsqrt(dval.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)).to(torch.bfloat16).float()
+    for rin in (None, torch.zeros_like(resid)):        # the accumulator alone, or + zero fp32 rows
+        out = torch.empty(M, 512, dtype=torch.bfloat16, device="cuda")
+        fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=rin, fx=fx, nsplit=0, norm_w=w, eps=1e-6)
+        ops.gemm_fused(None, frag_pack(W), out, fa, epi=ops.EPI_BF16 | ops.W_FRAG, M=M)
+        assert err(out, xn @ W.float().t()) < 1e-2
+    # FIN: fx + x.W^T into res (whose old rows are garbage), fx cleared
     tiles = N2 // 16
     x2, W2 = rnd(M, K2, seed=36), rnd(N2, K2, scale=1 / 64, seed=37)
-    res = resid.clone()
+    res = torch.full((M, H), 1e3, device="cuda")
     cnt = torch.zeros(tiles, dtype=torch.int32, device="cuda")
     ss = torch.zeros(M, tiles, device="cuda")
     xq = torch.empty(M, N2, dtype=torch.bfloat16, device="cuda")
@@ -1070,6 +1075,6 @@ def test_fx_accumulator_consumers_rmsnorm_and_fin_clear(M):
     fa = ops.fused_args(fin_cnt=cnt, fin_resid=res, ss_out=ss, ss_ld=tiles, fin_x=xq, norm_w=w, fx=fx)
     ops.gemm_fused(x2, frag_pack(W2), part, fa, epi=ops.EPI_F32_FIN | ops.W_FRAG, M=M, ksplit=ks)
     torch.cuda.synchronize()
-    ref = resid + dval + x2.float() @ W2.float().t()
+    ref = dval + x2.float() @ W2.float().t()
     assert err(res, ref) < 1e-4
     assert int(fx.abs().sum()) == 0 and int(cnt.abs().sum()) == 0
