@@ -69,8 +69,16 @@ struct GemvIdx {
 };
 
 #ifndef PG_GEMV_PRO_EARLY
-#define PG_GEMV_PRO_EARLY 2     // 2: the q|k|v GEMV at M == 1; 1: gate/up too (152 VGPRs: 3 waves/SIMD); 0: off
+#define PG_GEMV_PRO_EARLY 2     // 2: the q|k|v GEMV at M == 1; 1: gate/up too (152 VGPRs: 3 waves/SIMD, level); 0: off
+                                // (measured and removed: the same loads as LDS DMA, slower; the o_proj merge prologue's
+                                // partials loaded early, level -- profiles/r05_decode_early_prologue_ab.jsonl)
 #endif
+// A workgroup barrier that orders LDS only: the wave's LDS ops are waited for, its global loads (the weight ring) stay
+// in flight (__syncthreads' fence would wait for them too: s_waitcnt vmcnt(0))
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
 // The batch-1 RMSNorm prologue in two halves (PRO 1, M == 1, K <= 2048): the loads -- thread t owns the float4s
 // c = t and t + 256 of the row, the residual's and the norm weight's, the fixed-point accumulator's raw words --
 // and, after the weight ring is issued, the sum of squares, the normalisation and the LDS image.
@@ -110,7 +118,7 @@ __device__ __forceinline__ void pro1_row_finish(const PgFusedArgs& f, int K, con
   }
   ss = wave_sum(ss);
   if ((t & 63) == 0) red[t >> 6] = ss;
-  __syncthreads();
+  lds_barrier();
   const float rstd = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + f.eps);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -123,7 +131,7 @@ __device__ __forceinline__ void pro1_row_finish(const PgFusedArgs& f, int K, con
       *(u32x2*)(xs + c * 4) = pk;
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 template <int PRO>
@@ -446,8 +454,10 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
                      M == 1 && (K >> 2) <= 512 && e.f.nsplit == 0 &&
                      e.f.resid_out == nullptr;
   Pro1Row p1;
-  if constexpr (PRO == 1 && PG_GEMV_PRO_EARLY)
+  if constexpr (PRO == 1 && PG_GEMV_PRO_EARLY) {
     if (early) pro1_row_load(e.f, K, p1);
+    __builtin_amdgcn_sched_barrier(0);         // (the prologue's loads stay ahead of the ring in the vmcnt order)
+  }
   // weights issued before the prologue (its loads are the critical path: the stream overlaps them)
   constexpr bool prew = STAGED && PG_GEMV_PREW;
   if (prew) {
