@@ -37,11 +37,14 @@
 #ifndef PG_GEMV_D2
 #define PG_GEMV_D2 4
 #endif
-#ifndef PG_GEMV_GU_NT
-#define PG_GEMV_GU_NT 2   // tuning: 4 = gate/up GEMV at M <= 2 with four 16-row tiles (two gate/up pairs) per workgroup
+// (round 5: the gate/up GEMV at batch 1 with two gate/up pairs per workgroup -- half the workgroups re-reading the row
+// -- measured slower, 1.061 vs 1.059 ms/token at 3 chunks in flight, 1.073 at 2: profiles/r05_gateup_nt4_ab.jsonl)
+#ifndef PG_GEMV_LM_NT
+#define PG_GEMV_LM_NT 2   // the batch-1..4 lm_head GEMV with two 16-row tiles per workgroup (1: one; 2 with 6 chunks in
+                          // flight: -5.5 us per token, 4 chunks: -3.5, profiles/r05_lm_head_nt2_ab.jsonl)
 #endif
-#ifndef PG_GEMV_GU_D
-#define PG_GEMV_GU_D 3    // ... and that form's chunks in flight
+#ifndef PG_GEMV_LM_D
+#define PG_GEMV_LM_D 6    // ... and that form's chunks in flight
 #endif
 #ifndef PG_GEMV_D1
 #define PG_GEMV_D1 8      // chunks in flight of the one-tile GEMV (M <= 4: batch-1 decode o / down / q|k|v / lm_head)
@@ -809,9 +812,9 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   // (four tiles per workgroup at 5..16 rows -- x's share of a workgroup's bytes 1/5 instead of 1/3 -- measured
   // slower on the pt-448 x16 gate/up and finalised down: 1.408 vs 1.380 ms/step; the epilogues take any even NT)
   // ring depths re-checked on the final round-2 code: two-tile kernels 4 chunks in flight, one-tile 8
-  if constexpr (PG_GEMV_GU_NT == 4 && EPI == PG_EPI_BF16_GELU_MUL) {
-    if (e.M <= 2 && ntiles % 4 == 0) {    // (tuning) two gate/up pairs per workgroup at batch 1-2: half the row re-reads
-      launch_gemv_cpw<EPI, 4, PG_GEMV_GU_D, PRO, FRAG>(dim3(ntiles / 4, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
+  if constexpr (PG_GEMV_LM_NT == 2 && EPI == PG_EPI_F32) {
+    if (e.M <= 4 && ntiles >= 8192 && ksplit == 1) {   // (tuning) the lm_head at batch 1-4 with two tiles per workgroup
+      launch_gemv_cpw<EPI, 2, PG_GEMV_LM_D, PRO, FRAG>(dim3((ntiles + 1) / 2, 1), lds, st, A, lda, W, ldw, K, 1, e);
       return;
     }
   }

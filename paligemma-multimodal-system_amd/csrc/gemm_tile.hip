@@ -485,6 +485,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
 // Split-K finalisation for the bf16 epilogues (prefill at small M, where a full-K tile grid leaves CUs
 // idle): the GEMM writes fp32 slabs [z][M][N] (bias in slab 0), this kernel sums them and applies the
 // epilogue (bf16 / gelu / gelu*up / V^T side output / RoPE + KV-cache append).  One thread per 4 outputs.
+#ifndef PG_FIN_ROPE_EARLY
+#define PG_FIN_ROPE_EARLY 1
+#endif
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restrict__ part, int nsplit, EpiArgs e) {
   const int NO = EPI == PG_EPI_BF16_GELU_MUL ? e.N / 2 : e.N;     // output columns
@@ -502,8 +505,23 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
     // output column c0 <- gate column 32*(c0/16) + c0%16, up column +16
     const int gb = (c0 / 16) * 32, q = c0 % 16;
     epi_gelu_mul4(e, m, gb, q, sum4(gb + q), sum4(gb + 16 + q));
-  } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+  } else if constexpr (EPI == PG_EPI_QKV_ROPE && !PG_FIN_ROPE_EARLY) {
     epi_qkv_rope4_pr(e, m, c0, sum4(c0), sum4(c0 ^ 8));
+  } else if constexpr (EPI == PG_EPI_QKV_ROPE) {
+    // the rotary position and cache slot are loaded before the slabs and the cos / sin right after them: two memory
+    // round trips instead of three (slabs, then the position, then the table)
+    bool roped;
+    const int ii = rope_freq_index(e.f, c0, &roped);
+    const int p = e.f.pos[m];
+    const int slot0 = e.f.slot_base + (e.f.slot_dev ? *e.f.slot_dev : 0);
+    const f32x4 v = sum4(c0), pr = sum4(c0 ^ 8);
+    f32x4 cs = {1.f, 1.f, 1.f, 1.f}, sn = {0.f, 0.f, 0.f, 0.f};
+    if (roped) {
+      const long off = (long)p * (e.f.head_dim >> 1) + ii;
+      cs = *(const f32x4*)(e.f.cos_t + off);
+      sn = *(const f32x4*)(e.f.sin_t + off);
+    }
+    epi_qkv_rope4_core(e, m, c0, v, pr, cs, sn, slot0);
   } else {
     EpiArgs e2 = e;
     e2.bias = nullptr;                                            // already in slab 0

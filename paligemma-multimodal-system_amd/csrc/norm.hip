@@ -10,6 +10,9 @@
 #include "common.h"
 
 #define NORM_MAXV 4   // float4 per thread -> H <= 4096
+#ifndef PG_NORM_W_EARLY
+#define PG_NORM_W_EARLY 1   // norm weights / bias loaded with the residual (not after the reductions)
+#endif
 // Split-K slabs loaded per round (SG) and float4 slots per thread (MAXV) are template parameters: 8 slabs per round
 // pays where few rows carry many slabs (batch-1 prefill: 16-slab down projection), but its 214 registers (two
 // waves per SIMD) tripled the 16 k-row norms of pt-448 x16 (55 -> 151 us each, 85 -> 93 ms per prefill): large
@@ -31,6 +34,16 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   const int nv = (H4 + 255) >> 8;                  // float4 slots in use per thread (wave-uniform)
   float* x = resid + (size_t)row * H;
   f32x4 v[MAXV];
+  // the norm weights (and LayerNorm bias) are loaded with the residual, not after the reductions: one dependent
+  // round trip fewer at the end of every launch
+  f32x4 wv[MAXV], bv[MAXV];
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i)
+    if (PG_NORM_W_EARLY && i < nv) {
+      const int c = min((int)threadIdx.x + i * 256, H4 - 1);
+      wv[i] = ((const f32x4*)w)[c];
+      bv[i] = mode == 0 ? ((const f32x4*)b)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   // the residual and the split-K slabs, NORM_SG slabs per round with every load of a round issued before the
   // first add (columns past H re-read the last column, dropped after the loads): one memory round trip per round
   // instead of one per slab (the runtime-bounded add loop waited for each slab's load before issuing the next --
@@ -94,15 +107,17 @@ __global__ __launch_bounds__(256) void norm_residual_kernel(float* __restrict__ 
   for (int i = 0; i < MAXV; ++i) {
     const int c = threadIdx.x + i * 256;
     if (c < H4) {
-      const f32x4 wv = ((const f32x4*)w)[c];
       f32x4 y;
+      if (!PG_NORM_W_EARLY) {
+        wv[i] = ((const f32x4*)w)[c];
+        bv[i] = mode == 0 ? ((const f32x4*)b)[c] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       if (mode == 0) {
-        const f32x4 bv = ((const f32x4*)b)[c];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * wv[j] + bv[j];
+        for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * wv[i][j] + bv[i][j];
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) y[j] = (v[i][j] * rstd) * (1.0f + wv[j]);
+        for (int j = 0; j < 4; ++j) y[j] = (v[i][j] * rstd) * (1.0f + wv[i][j]);
       }
       if constexpr (Q8) {
 #pragma unroll
