@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 11: PgFusedArgs mx_out / mx_in (MX block-scaled fp8 decode MLP rows); 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -111,6 +111,15 @@ typedef struct PgFusedArgs {
                                the finalised residual is fx + slabs (written to fin_resid, whose old rows are not
                                read), and the launch leaves fx zero (each tile's finalising workgroup clears its
                                entries)                                                                           */
+  /* ABI 11 -- MX (OCP microscaling) rows for the batched fp8 decode MLP: one E8M0 scale per 32 k, no quantiser launch */
+  uint8_t* mx_out;          /* PG_EPI_BF16_GELU_MUL with PG_FP8|PG_W_FRAG, M <= 32, ksplit 1, (N/2) % 128 == 0: C is
+                               written as e4m3 bytes [M][ldc bytes] of h = bf16(gelu(gate)*up) / 2^e, and mx_out
+                               [M][4][N/256] the E8M0 byte e + 127 of each 32-column block kb at [m][kb % 4][kb / 4],
+                               e = the smallest exponent with max|h| of the block <= 448 * 2^e (0 for a zero block),
+                               clamped to [-127, 127] (e4m3 RNE of h / 2^e)                                          */
+  const uint8_t* mx_in;     /* PG_EPI_F32 with PG_FP8|PG_W_FRAG, M <= 32, pro_mode 0: A is e4m3 [M][lda] with
+                               mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale is
+                               not read                                                                           */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -124,6 +133,9 @@ typedef struct PgFusedArgs {
  * C[m][n] is multiplied by a_scale[m] * w_scale[n] before the epilogue (bias, gelu*mul, RoPE/KV, fp32 slabs).
  * 16x16x128 block-scaled MFMA with unit block scales (2x the bf16 rate).  M > 16, K % 128 == 0, lda and ldw
  * multiples of 16, no prologue, epi in {BF16, BF16_GELU_MUL, F32, QKV_ROPE}. */
+/* With PG_W_FRAG the fp8 W is packed per 16-row block t and 128-wide k chunk c as W[16t + r][128c + 64s + 16g + e]
+ * (r, e < 16, g < 4, s < 2) at byte ((((t * K/128 + c) * 2 + s) * 4 + g) * 16 + r) * 16 + e (pghip/weights.py
+ * frag_pack8): the 16x16x128 MFMA's own k order. */
 #define PG_FP8 0x200
 /* PG_TILE_M1 (bf16 tile GEMMs, 256 <= M <= 288: batch-1 prefill, 256 image rows + the prompt): all M rows
  * in ONE row tile per 128 output columns, so each weight tile streams from HBM once (the 256x256 tiling

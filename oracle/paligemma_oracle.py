@@ -54,22 +54,43 @@ class bf16_operands:
 # model then bounds the HIP fp8 path's distance to the fp32 reference.  The tied lm_head: the HIP path runs it in e4m3
 # for 17..32-row batches (engine._lm_gemm, the fp8 GEMV) and in bf16 otherwise; lm_head=True emulates the e4m3 form
 # (tests/golden/make_emu.py sets it for the batch-32 fixtures).
+# mx_h=True: a down_proj call of at most 32 rows (batched decode) takes MX rows instead -- h rounded to bf16, then
+# e4m3 with one power-of-two scale per 32 contiguous columns (engine.MX_H: the gate/up epilogue's mx_out rule,
+# csrc/common.h mx_exp), the weights per-channel as before.
 _FP8_MIN_ROWS = None
 _FP8_LM_HEAD = False
+_FP8_MX_H = False
 
 
 class fp8_operands:
-    def __init__(self, min_rows: int = 16, lm_head: bool = False):
-        self.min_rows, self.lm_head = min_rows, lm_head
+    def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False):
+        self.min_rows, self.lm_head, self.mx_h = min_rows, lm_head, mx_h
 
     def __enter__(self):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD
-        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD)
-        _FP8_MIN_ROWS, _FP8_LM_HEAD = self.min_rows, self.lm_head
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H
+        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H)
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H = self.min_rows, self.lm_head, self.mx_h
 
     def __exit__(self, *a):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD
-        _FP8_MIN_ROWS, _FP8_LM_HEAD = self._old
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H = self._old
+
+
+def mx_exp(amax: np.ndarray) -> np.ndarray:
+    """E8M0 exponent per block: the smallest e with amax <= 448 * 2^e (0 for a zero block), clamped to [-127, 127]
+    (test aid mirroring csrc/common.h mx_exp: amax = f * 2^k, f in [0.5, 1) -> k - 9, or k - 8 when f * 512 > 448)."""
+    f, k = np.frexp(amax.astype(F32))
+    e = k - 9 + (f * F32(512.0) > F32(448.0)).astype(k.dtype)
+    return np.where(amax > 0, np.clip(e, -127, 127), 0).astype(np.int32)
+
+
+def mx_rows(x: np.ndarray) -> np.ndarray:
+    """MX round trip (block 32 along the last axis): x ~= e4m3(x / 2^e) * 2^e, e = mx_exp(block max |x|)."""
+    import torch
+    x2 = np.ascontiguousarray(x, dtype=F32).reshape(-1, x.shape[-1] // 32, 32)
+    sc = np.ldexp(F32(1.0), mx_exp(np.abs(x2).max(axis=2, keepdims=True))).astype(F32)
+    q = torch.from_numpy(x2 / sc).to(torch.float8_e4m3fn).float().numpy()
+    return (q * sc).reshape(x.shape).astype(F32)
 
 
 def q8_rows(x: np.ndarray) -> np.ndarray:
@@ -115,10 +136,14 @@ def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float) -> np.nd
     return (y * w + b).astype(F32)
 
 
-def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: bool = False) -> np.ndarray:
-    """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation.)"""
-    if gemma and _FP8_MIN_ROWS is not None and x.size // x.shape[-1] > _FP8_MIN_ROWS:
-        y = q8_rows(x) @ q8_rows(w).T
+def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: bool = False,
+           mx: bool = False) -> np.ndarray:
+    """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation; mx: the down_proj,
+    whose <= 32-row calls take MX rows under fp8_operands(mx_h=True).)"""
+    rows = x.size // x.shape[-1]
+    if gemma and _FP8_MIN_ROWS is not None and rows > _FP8_MIN_ROWS:
+        xq = mx_rows(q16(x)) if (mx and _FP8_MX_H and rows <= 32) else q8_rows(x)
+        y = xq @ q8_rows(w).T
     else:
         y = q16(x) @ w.T
     if b is not None:
@@ -285,7 +310,7 @@ def gemma_mlp(W: dict, lp: str, x: np.ndarray) -> np.ndarray:
     """GemmaMLP.forward (modeling_gemma.py:210-218)."""
     y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"], gemma=True))
     u = linear(x, W[lp + "up_proj.weight"], gemma=True)
-    return linear(y * u, W[lp + "down_proj.weight"], gemma=True)
+    return linear(y * u, W[lp + "down_proj.weight"], gemma=True, mx=True)
 
 
 def gemma_model(W: dict, tcfg: dict, input_embeds: np.ndarray, position_ids, mask, kv_cache,

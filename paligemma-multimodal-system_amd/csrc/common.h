@@ -90,6 +90,38 @@ __device__ __forceinline__ f32x4 mfma8(const bf16x8& a0, const bf16x8& a1, const
   const i32x8 b = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
+// the same with a per-lane E8M0 block scale for B (MX rows: lane (r, g)'s 32 bytes are block g of row r of B)
+__device__ __forceinline__ f32x4 mfma8s(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0, const bf16x8& b1,
+                                        const f32x4& c, int sb) {
+  const i32x4 x0 = __builtin_bit_cast(i32x4, a0), x1 = __builtin_bit_cast(i32x4, a1);
+  const i32x4 y0 = __builtin_bit_cast(i32x4, b0), y1 = __builtin_bit_cast(i32x4, b1);
+  const i32x8 a = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const i32x8 b = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, sb);
+}
+// Pin finished MFMA accumulators in VGPRs here (straight-line, before any epilogue branch).  Without it the compiler may
+// sink a whole v_mfma_scale chain into the epilogue's first guarded block and read its first result register a few
+// SALU instructions after the last MFMA on the branch-skipping path -- before the MFMA has written it (measured: the
+// last chunk missing from element 0 of every lane of one row tile, profiles/r05_mfma_sink_hazard.txt)
+// (16 extra wait states on top of the hazard recognizer's own, once per kernel)
+template <int N>
+__device__ __forceinline__ void mfma_fence(f32x4 (&a)[N]) {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 7");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(a[i]));
+  __builtin_amdgcn_sched_barrier(0);
+}
+// E8M0 exponent of an MX block whose max |x| is amax: the smallest e with amax <= 448 * 2^e (0 for a zero block),
+// clamped to [-127, 127].  amax = f * 2^k, f in [0.5, 1): f * 512 in [256, 512), so e = k - 9, or k - 8 when f > 7/8.
+__device__ __forceinline__ int mx_exp(float amax) {
+  if (!(amax > 0.f)) return 0;
+  int k;
+  const float f = frexpf(amax, &k);
+  const int e = k - 9 + (f * 512.f > 448.f ? 1 : 0);
+  return min(max(e, -127), 127);
+}
 __device__ __forceinline__ f32x4 mfma8(const i32x8& a, const i32x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }

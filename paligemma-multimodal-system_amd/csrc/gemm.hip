@@ -52,6 +52,9 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                         ldc >= N);
   if (epi == PG_EPI_FX_ADD) PG_REQUIRE(M <= 16 && !fp8 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N &&
                                        ((uintptr_t)C & 15) == 0 && ldc % 2 == 0);
+  if (f.mx_in) PG_REQUIRE(fp8 && frag && epi == PG_EPI_F32 && M <= 32 && f.pro_mode == 0 && K % 128 == 0 && A != nullptr);
+  if (f.mx_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.pro_mode == 0 && !f.amax_out && ksplit == 1 &&
+                           (N / 2) % 128 == 0 && PG_GEMV8_WIDE && ((K >> 7) + ksplit - 1) / ksplit * 128 <= 4096);
   if (f.fx) PG_REQUIRE(((uintptr_t)f.fx & 15) == 0 && (f.pro_mode == 1) != (epi == PG_EPI_F32_FIN) && !fp8 &&
                        M <= 16);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD || epi == PG_EPI_FX_ADD);
@@ -64,7 +67,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   const bf16_t* w = (const bf16_t*)W;
   if (fp8 && frag) {
     // fp8 weight-streaming GEMV (M <= 32): fp8 fragment-packed W (weights.frag_pack8), row-major e4m3 x
-    PG_REQUIRE(M <= 32 && (f.pro_mode == 0 || f.pro_mode == 5) && (f.a_scale || f.pro_mode == 5) && f.w_scale &&
+    PG_REQUIRE(M <= 32 && (f.pro_mode == 0 || f.pro_mode == 5) && (f.a_scale || f.pro_mode == 5 || f.mx_in) && f.w_scale &&
                K % 128 == 0 && N % 16 == 0 && ldw == K && lda >= K && (lda % 16 == 0 || f.pro_mode == 5) &&
                ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0 && epi != PG_EPI_F32_FIN);
     const int rc = pg_dispatch_gemv8(epi, (const uint8_t*)A, lda, (const uint8_t*)W, K, ksplit, e, stream);

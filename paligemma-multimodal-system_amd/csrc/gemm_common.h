@@ -140,6 +140,14 @@ struct PgFusedArgs {
   // fx + slabs (fin_resid is written, not read) and clears the fx entries it finalised (the accumulator is zero again
   // once the FIN launch ends)
   long long* fx;
+  // ABI 11, MX (OCP microscaling) fp8 rows for the 17..32-row fp8 decode MLP: E8M0 scales, one per 32 consecutive k of
+  // a row, stored [M][4][K/128] (row m's block g of 128-k chunk c at m*K/32 + g*K/128 + c: a lane's scales for the
+  // chunks of its K split are consecutive bytes).  mx_out (gate/up: PG_EPI_BF16_GELU_MUL with PG_FP8|PG_W_FRAG): C is
+  // the e4m3 h [M][ldc] bytes and mx_out its scales -- x = q * 2^(s - 127); mx_in (a PG_FP8|PG_W_FRAG consumer, the
+  // down projection): A holds such rows and mx_in their scales, fed to the MFMA as its per-lane block scales (a_scale
+  // is not read)
+  uint8_t* mx_out;
+  const uint8_t* mx_in;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)
@@ -180,7 +188,7 @@ struct EpiArgs {
 // fp8 dequantisation of one accumulator fragment: C[m][n0..n0+3] *= a_scale[m] * w_scale[n0..n0+3]
 __device__ __forceinline__ void scale_acc(const EpiArgs& e, int m, int n0, f32x4& v) {
   if (m >= e.M || n0 >= e.N) return;
-  v *= e.f.a_scale[m] * load4_guard(e.f.w_scale, n0, e.N);
+  v *= (e.f.mx_in ? 1.0f : e.f.a_scale[m]) * load4_guard(e.f.w_scale, n0, e.N);   // (MX rows: scaled in the MFMA)
 }
 
 // RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are

@@ -9,11 +9,15 @@
 // W through LDS at 3.1-3.3 TB/s.  Here, as in gemv_body, W streams straight to VGPRs: the weights are stored
 // fragment-packed (PG_W_FRAG with PG_FP8, weights.frag_pack8): W[16t + r][128c + 64s + 16g + e] (e < 16 bytes) at
 // byte ((t * (K/128) + c) * 2 + s) * 1024 + (16g + r) * 16 + e, so piece s of a 16-row x 128-k chunk is one 1-KiB
-// lane-linear non-temporal load.  Lane (r, g) loads x row r (and 16 + r) at the same k bytes, one
+// lane-linear non-temporal load -- the MFMA's own k order (lane group g holds k 16g + e and 64 + 16g + e; measured,
+// scripts/tune/mx_probe.hip).  Lane (r, g) loads x row r (and 16 + r) at the same k bytes, one
 // v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per (W tile, 16-row x tile) and chunk; the 4 waves split
 // the chunks of split blockIdx.y round-robin, DEPTH chunks in flight, and reduce through LDS.  The accumulator is
 // scaled by a_scale[m] * w_scale[n] before the tile kernel's epilogues (bf16, gelu*up, fp32 slabs, RoPE + KV).
-template <int EPI, int NT, int MT, int DEPTH, int CPW>
+// MX: x rows carry E8M0 block scales (PgFusedArgs.mx_in, [M][4][K/128]).  The MFMA takes the scale of column r's
+// 32-k block b (k 32b .. 32b + 31 of the chunk, spread over lane groups 2(b % 2) and 2(b % 2) + 1) from lane (r, b), so
+// lane (r, g) loads block g's scale byte with its x bytes (no a_scale in the epilogue)
+template <int EPI, int NT, int MT, int DEPTH, int CPW, bool MX = false>
 __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ X, int ldx,
                                                     const uint8_t* __restrict__ W, int K, EpiArgs e) {
   amax_clear(e);
@@ -40,8 +44,17 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[t][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   u32x4 wb[DEPTH][NT][2], xb[DEPTH][MT][2];
-  auto load = [&](int j, u32x4 (&wv)[NT][2], u32x4 (&xv)[MT][2]) {
+  int sbr[DEPTH][MT];
+  const uint8_t* mxr[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+    mxr[mt] = MX ? e.f.mx_in + (size_t)min(mt * 16 + r, M - 1) * (K >> 5) + (size_t)g * nch_all : nullptr;
+  auto load = [&](int j, u32x4 (&wv)[NT][2], u32x4 (&xv)[MT][2], int (&sv)[MT]) {
     const size_t cc = (size_t)(c0 + wave + j * 4);
+    if constexpr (MX) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) sv[mt] = mxr[mt][cc];
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -52,25 +65,28 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) xv[mt][sp] = *(const u32x4*)(xr[mt] + cc * 128 + sp * 64);
   };
-  auto compute = [&](const u32x4 (&wv)[NT][2], const u32x4 (&xv)[MT][2]) {
+  auto compute = [&](const u32x4 (&wv)[NT][2], const u32x4 (&xv)[MT][2], const int (&sv)[MT]) {
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]),
-                           __builtin_bit_cast(bf16x8, xv[mt][0]), __builtin_bit_cast(bf16x8, xv[mt][1]), acc[t][mt]);
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[t][0]), w1 = __builtin_bit_cast(bf16x8, wv[t][1]);
+        const bf16x8 x0 = __builtin_bit_cast(bf16x8, xv[mt][0]), x1 = __builtin_bit_cast(bf16x8, xv[mt][1]);
+        if constexpr (MX) acc[t][mt] = mfma8s(w0, w1, x0, x1, acc[t][mt], sv[mt]);
+        else acc[t][mt] = mfma8(w0, w1, x0, x1, acc[t][mt]);
+      }
   };
   // (QKV epilogue operands issued with the stream, as gemv_body does, are not needed: the tile epilogue loads them)
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
-    if (CPW > 0 ? d < CPW : d < mine) load(d, wb[d], xb[d]);
+    if (CPW > 0 ? d < CPW : d < mine) load(d, wb[d], xb[d], sbr[d]);
   if constexpr (CPW > 0) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < CPW; ++j) {
       const int d = j % DEPTH;
-      compute(wb[d], xb[d]);
-      if (j + DEPTH < CPW) load(j + DEPTH, wb[d], xb[d]);
+      compute(wb[d], xb[d], sbr[d]);
+      if (j + DEPTH < CPW) load(j + DEPTH, wb[d], xb[d], sbr[d]);
       __builtin_amdgcn_sched_barrier(0);
     }
   } else {
@@ -79,12 +95,14 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
       for (int d = 0; d < DEPTH; ++d) {
         const int j = base + d;
         if (j < mine) {
-          compute(wb[d], xb[d]);
-          if (j + DEPTH < mine) load(j + DEPTH, wb[d], xb[d]);
+          compute(wb[d], xb[d], sbr[d]);
+          if (j + DEPTH < mine) load(j + DEPTH, wb[d], xb[d], sbr[d]);
         }
       }
     }
   }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) mfma_fence(acc[t]);
   __shared__ f32x4 red[4][NT][MT][64];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -128,11 +146,17 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 // thread loads 16-element pieces, divides by s[m] = amax / 448 and packs e4m3 (pg_quant_fp8's bytes) into the same
 // swizzled LDS layout -- the quantiser launch between gate/up and down is gone; x costs twice the bytes per
 // workgroup (bf16), all issued before the W stream.
-template <int EPI, int NTW, int MT, int DEPTH, int CPW, bool XB = false>
+// MX (CPW > 0): x rows carry E8M0 block scales (PgFusedArgs.mx_in): lane (r, g)'s scale bytes (block g of each of
+// the CPW chunks of its split, as in gemv8_kernel) are loaded before the W stream and handed to the MFMA per chunk.
+// GELU_MUL with PgFusedArgs.mx_out (NTW 2: a wave's gate/up pair is 16 h columns, waves w and w ^ 1 hold the two halves
+// of a 32-column MX block): h is written as e4m3 bytes with one E8M0 scale per block -- the block max of the
+// bf16-rounded h exchanged between the two waves through LDS, no cross-workgroup reduction and no quantiser launch.
+template <int EPI, int NTW, int MT, int DEPTH, int CPW, bool XB = false, bool MX = false>
 __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__ X, int ldx,
                                                      const uint8_t* __restrict__ W, int K, EpiArgs e) {
   extern __shared__ __attribute__((aligned(16))) char xs8[];
   static_assert(!XB || CPW > 0, "the bf16-x form needs a compile-time chunk count");
+  static_assert(!MX || (CPW > 0 && !XB), "MX rows need a compile-time chunk count");
   amax_clear(e);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -167,6 +191,17 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       const int lc = pc ^ (row & 7);
       const uint8_t* src = X + (size_t)min(row, M - 1) * ldx + (size_t)c0 * 128 + lc * 16;
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(xs8 + pi * 1024), 16, 0, 0);
+    }
+  }
+  // MX rows: this lane's E8M0 scale of block g of each of its CPW chunks, rows r and 16 + r (loaded with the x pieces,
+  // before the W stream; the step-3 wait covers them)
+  int sbx[MX ? MT : 1][MX ? CPW : 1];
+  if constexpr (MX) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const uint8_t* sp = e.f.mx_in + (size_t)min(mt * 16 + r, M - 1) * (K >> 5) + (size_t)g * nch_all + c0;
+#pragma unroll
+      for (int j = 0; j < CPW; ++j) sbx[mt][j] = sp[j];
     }
   }
   // the x DMA pieces stay ahead of every W load in the vmcnt order (step 3 waits for "at most the W loads
@@ -223,16 +258,21 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       const int row = mt * 16 + r;
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
-        const int lc = j * 8 + sp * 4 + g;
+        const int lc = j * 8 + sp * 4 + g;           // the lane's 16-B pieces: k 64sp + 16g of chunk j
         xf[mt][sp] = *(const bf16x8*)(xs8 + row * Kr + ((lc ^ (row & 7)) << 4));
       }
     }
 #pragma unroll
     for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
-                           xf[mt][1], acc[t][mt]);
+      for (int mt = 0; mt < MT; ++mt) {
+        if constexpr (MX)
+          acc[t][mt] = mfma8s(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
+                              xf[mt][1], acc[t][mt], sbx[mt][MX ? j : 0]);
+        else
+          acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
+                             xf[mt][1], acc[t][mt]);
+      }
   };
   if constexpr (CPW > 0) {
     __builtin_amdgcn_sched_barrier(0);
@@ -255,8 +295,11 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       }
     }
   }
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) mfma_fence(acc[t]);
   const int q = 4 * g;
-  float gam[MT];                                   // GELU_MUL with amax_out: this lane's max |h| per row tile
+  float gam[MT];                                   // GELU_MUL with amax_out / mx_out: this lane's max |h| per row tile
+  f32x4 mxh[MT];                                   // ... mx_out: the lane's h values
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
@@ -274,7 +317,16 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       for (int t = 0; t < NTW; ++t) scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
     }
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
-      if (e.f.amax_out) {
+      if (NTW == 2 && e.f.mx_out) {
+        // MX h: the lane's 4 bf16-rounded values kept for the block scale below (stored there)
+        const f32x4 gv = acc[0][mt], uv = acc[1][mt];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float hv = __uint_as_float((uint32_t)f2bf(gelu_tanh(gv[j]) * uv[j]) << 16);
+          mxh[mt][j] = hv;
+          gam[mt] = fmaxf(gam[mt], fabsf(hv));
+        }
+      } else if (e.f.amax_out) {
 #pragma unroll
         for (int t = 0; t < NTW; t += 2)
           gam[mt] = fmaxf(gam[mt], epi_gelu_mul4_amax(e, m, (tile0 + t) * 16, q, acc[t][mt], acc[t + 1][mt]));
@@ -288,6 +340,36 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
     } else {
 #pragma unroll
       for (int t = 0; t < NTW; ++t) epi_store4<EPI>(e, m, (tile0 + t) * 16 + q, acc[t][mt], z);
+    }
+  }
+  if constexpr (EPI == PG_EPI_BF16_GELU_MUL && NTW == 2) {
+    if (e.f.mx_out) {                              // (uniform: every wave reaches the barrier)
+      // block max over the 4 lanes of a row (16 columns), then with the partner wave's 16 (the block's other half)
+      __shared__ float smx[4][16 * MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float v = gam[mt];
+        v = fmaxf(v, __shfl_xor(v, 16, 64));
+        v = fmaxf(v, __shfl_xor(v, 32, 64));
+        gam[mt] = v;
+        if (g == 0) smx[wave][mt * 16 + r] = v;
+      }
+      __syncthreads();
+      const int pair = tile0 >> 1, kb = pair >> 1;  // this wave's 16 h columns [16 pair, +16) lie in 32-block kb
+      const int Nh = e.N >> 1;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int m = mt * 16 + r;
+        const int ex = mx_exp(fmaxf(gam[mt], smx[wave ^ 1][mt * 16 + r]));
+        const float inv = __builtin_ldexpf(1.0f, -ex);
+        const int col = pair * 16 + q;
+        if (m < e.M && col + 3 < Nh) {
+          *(uint32_t*)((uint8_t*)e.C + (size_t)m * e.ldc + col) =
+              pack_fp8x4(mxh[mt][0] * inv, mxh[mt][1] * inv, mxh[mt][2] * inv, mxh[mt][3] * inv);
+          if ((wave & 1) == 0 && g == 0)
+            e.f.mx_out[(size_t)m * (Nh >> 5) + (size_t)(kb & 3) * (Nh >> 7) + (kb >> 2)] = (uint8_t)(ex + 127);
+        }
+      }
     }
   }
   if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
@@ -332,6 +414,17 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
       return;
     }
   }
+  if constexpr (EPI == PG_EPI_F32) {
+    if (e.f.mx_in) {                               // MX rows (launch_gemv8 checked: exact, 8 or 16 chunks)
+      if (per_z == 16)
+        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
+                           e);
+      else
+        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 8, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
+                           e);
+      return;
+    }
+  }
   if (exact && per_z == 16)
     hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
   else if (exact && per_z == 8)
@@ -343,7 +436,7 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
 #ifndef PG_GEMV8_DEPTH
 #define PG_GEMV8_DEPTH 4
 #endif
-template <int EPI, int NT, int MT>
+template <int EPI, int NT, int MT, bool MX = false>
 static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
   const dim3 grid(((e.N >> 4) + NT - 1) / NT, ksplit);
@@ -351,16 +444,23 @@ static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, 
   const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
   constexpr int D = PG_GEMV8_DEPTH;                // chunks in flight per wave
   switch (cpw) {
-    case 2: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, 2, 2>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    case 4: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 4>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    case 8: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 8>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    default: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 0>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 2: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, 2, 2, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 4: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 4, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 8: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 8, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    default: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 0, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
   }
 }
 
 template <int EPI, int NT>
 static void launch_gemv8_nt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
+  if constexpr (EPI == PG_EPI_F32) {
+    if (e.f.mx_in) {
+      if (e.M <= 16) launch_gemv8_mt<EPI, NT, 1, true>(X, ldx, W, K, ksplit, e, st);
+      else launch_gemv8_mt<EPI, NT, 2, true>(X, ldx, W, K, ksplit, e, st);
+      return;
+    }
+  }
   if (e.M <= 16)
     launch_gemv8_mt<EPI, NT, 1>(X, ldx, W, K, ksplit, e, st);
   else
@@ -393,8 +493,10 @@ static void launch_gemv8(const uint8_t* X, int ldx, const uint8_t* W, int K, int
       return;
     }
   }
+  // (MX rows take the wide form only when its chunk count is a compile-time 8 or 16)
+  const bool mx_ok = !e.f.mx_in || ((K >> 7) % ksplit == 0 && (per_z == 8 || per_z == 16));
   if constexpr (EPI != PG_EPI_QKV_ROPE) {
-    if (PG_GEMV8_WIDE && per_z * 128 <= 4096) {
+    if (PG_GEMV8_WIDE && per_z * 128 <= 4096 && mx_ok) {
       const int wgs2 = (tiles + 7) / 8 * ksplit, wgs1 = (tiles + 3) / 4 * ksplit;
       if (e.M <= 16) {
         if (wgs2 >= 256 || EPI == PG_EPI_BF16_GELU_MUL) { launch_gemv8x_mt<EPI, 2, 1>(X, ldx, W, K, ksplit, e, st); return; }

@@ -28,7 +28,8 @@ class PgFusedArgs(C.Structure):
                 ("akeys", C.c_int), ("a_scale", C.c_void_p), ("w_scale", C.c_void_p),
                 ("slab_rows", C.c_int), ("kd", C.c_void_p), ("vd", C.c_void_p),
                 ("amax_out", C.c_void_p), ("amax_in", C.c_void_p), ("amax_ld", C.c_int), ("amax_zero", C.c_void_p),
-                ("amax_zero_n", C.c_int), ("fx", C.c_void_p)]
+                ("amax_zero_n", C.c_int), ("fx", C.c_void_p),
+                ("mx_out", C.c_void_p), ("mx_in", C.c_void_p)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -77,7 +78,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 def source_hash(lib=None) -> str:

@@ -132,6 +132,11 @@ class PaliGemmaEngine:
     # atomics; the quantiser it removes costs 7.3 us), so off
     HQ_FUSED = os.environ.get("PG_HQ_FUSED", "0") != "0"
 
+    # 17..32-row fp8 decode MLP on MX rows: the gate/up epilogue writes h as e4m3 with one E8M0 scale per 32
+    # columns (PgFusedArgs.mx_out) and the down GEMV reads those block scales into its MFMAs (mx_in) -- no
+    # quantiser launch and no cross-workgroup row maximum (the block max stays inside one workgroup)
+    MX_H = os.environ.get("PG_MX_H", "1") != "0"
+
     AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
     # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
     # doubles instead (pt-896: 16 slabs of 8 chunks, as many x bytes per workgroup as the 8-slab fp8 route)
@@ -836,6 +841,12 @@ class PaliGemmaEngine:
         hq = (self.HQ_FUSED and self.FP8_GEMV and self._fp8_rows(B) and B <= 32 and not add
               and all(k in w.tl[0] for k in ("qkv_w8f", "gu_w8f", "down_w8f"))
               and ich % self.HQ_CHUNKS == 0 and part.shape[0] >= sdh)
+        I = h.shape[1]
+        mx = (self.MX_H and not hq and not add and self.FP8_GEMV and self._fp8_rows(B) and B <= 32
+              and "gu_w8f" in w.tl[0] and "down_w8f" in w.tl[0] and I % 128 == 0 and w.hidden <= 4096)
+        if mx:
+            h8 = self._buf("d_h8", (B, I), torch.uint8)
+            hs = self._buf("d_hs", (B * I // 32,), torch.uint8)
         if hq:
             amax = self._buf("d_hamax", (B * self.AMAX_LD,), torch.int32)
             fa_gu = ops.fused_args(amax_out=amax, amax_ld=self.AMAX_LD)
@@ -861,6 +872,13 @@ class PaliGemmaEngine:
                 self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B, fa=fa_gu)
                 ops.gemm8_hx(h, amax, self.AMAX_LD, Lw["down_w8f"], Lw["down_s8"], part, M=B, ksplit=sdh)
                 ns = self._allreduce_slabs(part, sdh)
+                continue
+            if mx:                                  # MX h: e4m3 + block scales straight from gate/up into down
+                x8, xs = xin
+                ops.gemm8(x8, xs, Lw["gu_w8f"], Lw["gu_s8"], h8, epi=ops.EPI_BF16_GELU_MUL, M=B, frag=True, mx_out=hs)
+                ops.gemm8(h8, None, Lw["down_w8f"], Lw["down_s8"], part, epi=ops.EPI_F32, M=B, ksplit=sd, frag=True,
+                          mx_in=hs)
+                ns = self._allreduce_slabs(part, sd)
                 continue
             self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B)
             if add:

@@ -107,21 +107,33 @@ def quant_fp8(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional
     return q, scale
 
 
-def gemm8(A8: torch.Tensor, a_scale: torch.Tensor, W8: torch.Tensor, w_scale: torch.Tensor, out: torch.Tensor, *,
-          epi: int = EPI_BF16, M: Optional[int] = None, bias: Optional[torch.Tensor] = None, ksplit: int = 1,
-          fa=None, frag: bool = False) -> torch.Tensor:
+def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w_scale: torch.Tensor,
+          out: torch.Tensor, *, epi: int = EPI_BF16, M: Optional[int] = None, bias: Optional[torch.Tensor] = None,
+          ksplit: int = 1, fa=None, frag: bool = False, mx_in: Optional[torch.Tensor] = None,
+          mx_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """fp8 GEMM: out = epilogue((A8 . W8^T) * a_scale[m] * w_scale[n]) (PG_FP8, pg_gemm_fused).  A8, W8 are
     uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE.
-    frag: W8 is fp8 fragment-packed (weights.frag_pack8) -> the weight-streaming fp8 GEMV, M <= 32."""
+    frag: W8 is fp8 fragment-packed (weights.frag_pack8) -> the weight-streaming fp8 GEMV, M <= 32.
+    MX rows (frag only): mx_in = A8's E8M0 block scales [M][4][K/128] (EPI_F32; a_scale None), mx_out = the
+    scales a gelu*up launch writes beside its e4m3 h (out uint8 [M][N/2])."""
     for t, n in ((A8, "A8"), (W8, "W8")):
         if t.dtype != torch.uint8 or not t.is_cuda or t.stride(1) != 1:
             raise ValueError(f"pghip.gemm8: {n} must be a row-major uint8 (e4m3) HIP tensor")
-    _chk(a_scale, torch.float32, "a_scale")
+    if mx_in is None:
+        _chk(a_scale, torch.float32, "a_scale")
     _chk(w_scale, torch.float32, "w_scale")
     M = A8.shape[0] if M is None else M
     N, K = W8.shape
     fa = fused_args() if fa is None else fa
-    fa.a_scale, fa.w_scale = a_scale.data_ptr(), w_scale.data_ptr()
+    fa.a_scale = a_scale.data_ptr() if a_scale is not None else None
+    fa.w_scale = w_scale.data_ptr()
+    for t, n, numel in ((mx_in, "mx_in", M * K // 32), (mx_out, "mx_out", M * N // 64)):
+        if t is None:
+            continue
+        if not frag or t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous() or t.numel() < numel:
+            raise ValueError(f"pghip.gemm8: {n} must be a contiguous uint8 HIP tensor of >= {numel} E8M0 scales "
+                             "(fragment-packed W8 only)")
+        setattr(fa, n, t.data_ptr())
     e = epi & 0xFF
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
     if frag:

@@ -55,7 +55,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == _lib.ABI_VERSION == 10
+    assert lib.pg_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_library_matches_source_tree():

@@ -972,6 +972,59 @@ def test_gemm8_hx_equals_the_quantiser_route(M, I, H, ks):
         assert torch.allclose(p0, p1, rtol=1e-5, atol=1e-5)
 
 
+def _mx_quant(h):
+    """Torch restatement of the MX rule (PgFusedArgs.mx_out, csrc/common.h mx_exp): per 32 columns e = the smallest
+    exponent with max |h| <= 448 * 2^e, bytes e4m3(h / 2^e), scales e + 127 stored [M][4][K/128] (block 4c + g at
+    [m][g][c])."""
+    M, K = h.shape
+    b = h.view(M, K // 32, 32)
+    amax = b.abs().amax(2)
+    f, k = torch.frexp(amax)
+    ex = (k - 9 + (f * 512 > 448).int()).clamp(-127, 127)
+    ex = torch.where(amax > 0, ex, torch.zeros_like(ex))
+    q = (b / torch.exp2(ex.float())[..., None]).to(torch.float8_e4m3fn).view(torch.uint8).reshape(M, K)
+    sc = (ex + 127).to(torch.uint8).view(M, K // 128, 4).permute(0, 2, 1).contiguous()
+    return q, sc.view(-1)
+
+
+def _mx_deq(q8, sc, M, K):
+    s = sc.view(M, 4, K // 128).permute(0, 2, 1).reshape(M, K // 32).float()
+    return (q8.view(torch.float8_e4m3fn).float().view(M, K // 32, 32) * torch.exp2(s - 127)[..., None]).view(M, K)
+
+
+@pytest.mark.parametrize("M,I,H,ks", [(32, 16384, 2048, 8), (32, 2048, 2048, 1), (17, 4096, 1024, 2),
+                                      (24, 2048, 512, 1), (9, 256, 512, 1), (32, 16384, 2048, 16)])
+def test_mx_h_gate_up_and_down(M, I, H, ks):
+    """The batched fp8 decode MLP on MX rows (ABI 11, engine.MX_H): the gate/up GEMV writes h as e4m3 bytes with one
+    E8M0 scale per 32 columns (mx_out) -- bit-identical to the torch MX rule applied to the bf16 gelu*up launch's h --
+    and the down GEMV reading those block scales into its MFMAs (mx_in; the wide and the K-split forms) equals a torch
+    fp32 matmul of the dequantised operands up to summation order; also on scales spread over 2^-10 .. 2^10."""
+    from pghip import ops
+    from pghip.weights import frag_pack8, quant_rows_fp8
+    x = rnd(M, H, seed=85)
+    Wgu, Wd = rnd(2 * I, H, scale=1 / math.sqrt(H), seed=86), rnd(H, I, scale=1 / math.sqrt(I), seed=87)
+    x8, xs = ops.quant_fp8(x)
+    gu8, gus = quant_rows_fp8(Wgu)
+    d8, ds = quant_rows_fp8(Wd)
+    gu8f, d8f = frag_pack8(gu8), frag_pack8(d8)
+    h0 = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(x8, xs, gu8f, gus, h0, epi=ops.EPI_BF16_GELU_MUL, frag=True)
+    h8 = torch.full((M, I), 0x55, dtype=torch.uint8, device="cuda")
+    hs = torch.full((M * I // 32,), 0x55, dtype=torch.uint8, device="cuda")
+    ops.gemm8(x8, xs, gu8f, gus, h8, epi=ops.EPI_BF16_GELU_MUL, frag=True, mx_out=hs)
+    q_ref, s_ref = _mx_quant(h0.float())
+    assert torch.equal(hs, s_ref)
+    assert torch.equal(h8, q_ref)
+    assert err(_mx_deq(h8, hs, M, I), h0.float()) < 0.07          # e4m3: 3 mantissa bits per block
+    # float64 reference: the MX rows' block magnitudes spread (gelu*up h, and random scales over 2^20) makes the fp32
+    # summation order show at ~6e-5 of the row max at K = 2048 for the K-split form
+    for scales, tol in ((hs, 1e-4), (torch.randint(117, 138, (M * I // 32,), dtype=torch.uint8, device="cuda"), 3e-4)):
+        ref = (_mx_deq(h8, scales, M, I).double() @ _deq(d8, ds).double().t()).float()
+        part = torch.empty(ks, M, H, dtype=torch.float32, device="cuda")
+        ops.gemm8(h8, None, d8f, ds, part, epi=ops.EPI_F32, ksplit=ks, frag=True, mx_in=scales)
+        assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
+
+
 @pytest.mark.parametrize("M,N,K,ks", [(16, 2048, 16384, 8), (16, 2048, 2048, 2), (8, 1024, 4096, 4), (16, 512, 1024, 1)])
 def test_gemv_fin_residual_xprime_and_pair_sums(M, N, K, ks):
     """PG_EPI_F32_FIN on the bf16 GEMV (5..16-row decode): the residual += x.W^T (+ bias) finalised in-kernel, x' =
