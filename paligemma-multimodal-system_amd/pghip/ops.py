@@ -286,6 +286,9 @@ def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
     _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
 
 
+DECODE_MAX_SPLITS = int(os.environ.get("PG_DECODE_MAX_SPLITS", "8"))
+
+
 def decode_plan(B: int, Hkv: int, kcap: int):
     """(nsplit, nw, nb) of pg_attn_decode for a batch of B rows over a static cache of kcap keys: 4 waves per split
     and at most 8 splits per (row, kv head), the rounds following from the cache length.  The last split's workgroup
@@ -294,7 +297,7 @@ def decode_plan(B: int, Hkv: int, kcap: int):
     5 x 4 x 2 13.1; pt-896 x32 8 x 4 x 5 31.9 vs 6 x 4 x 6 30.9, 16 x 4 x 3 37.8, 16 x 2 x 5 35.4."""
     nblk = kcap // 32
     nw = 4 if nblk >= 4 else 2
-    nsplit = max(1, min(8, nblk // nw))
+    nsplit = max(1, min(DECODE_MAX_SPLITS, nblk // nw))
     nb = -(-nblk // (nw * nsplit))
     return nsplit, nw, nb
 
