@@ -117,9 +117,10 @@ typedef struct PgFusedArgs {
                                [M][4][N/256] the E8M0 byte e + 127 of each 32-column block kb at [m][kb % 4][kb / 4],
                                e = the smallest exponent with max|h| of the block <= 448 * 2^e (0 for a zero block),
                                clamped to [-127, 127] (e4m3 RNE of h / 2^e)                                          */
-  const uint8_t* mx_in;     /* PG_EPI_F32 with PG_FP8|PG_W_FRAG, M <= 32, pro_mode 0: A is e4m3 [M][lda] with
-                               mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale is
-                               not read                                                                           */
+  const uint8_t* mx_in;     /* PG_FP8|PG_W_FRAG (any epilogue but F32_ADD), M <= 32, pro_mode 0: A is e4m3 [M][lda]
+                               with mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale
+                               is not read.  With ss_in (rows from pg_norm_residual_mx, ss_n = K/256, eps) the outputs
+                               are multiplied by the row's rstd = rsqrt(sum ss_in[m*ss_ld + i] / K + eps)            */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -261,6 +262,13 @@ int pg_quant_fp8(const void* x, int ldx, int M, int K, void* q, int ldq, float* 
 int pg_norm_residual_fp8(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                          const float* b, void* q, int ldq, float* scale, const int* row_map, int M_out,
                          int H, int mode, float eps, int write_resid, hipStream_t stream);
+/* (ABI 11) Gemma RMSNorm for MX fp8 consumers (GemmaRMSNorm modeling_gemma.py:165-182 split at rstd): x = resid +
+ * sum_s partials[s] (slab order; written back when write_resid), q uint8 [M][ldq] = e4m3 of y = x*(1+w) with one
+ * E8M0 scale per 32 columns in qs [M][4][H/128] (the PgFusedArgs.mx_out rule), ss [M][ss_ld] = sum of x^2 per 256
+ * columns.  The consumer (an fp8 GEMV with mx_in = qs, ss_in = ss, ss_n = H/256, eps) applies rstd to its outputs.
+ * H % 256 == 0; resid, partials, w 16-B aligned. */
+int pg_norm_residual_mx(float* resid, const float* partials, int nsplit, int M_part, const float* w, void* q,
+                        int ldq, void* qs, float* ss, int ss_ld, int M, int H, int write_resid, hipStream_t stream);
 
 /* ---- one-shot all-reduce over xGMI (the reference is single-device, so this
  * replaces nothing there -- it is the tensor-parallel exchange of the Gemma decoder's o_proj / down_proj

@@ -56,24 +56,28 @@ class bf16_operands:
 # (tests/golden/make_emu.py sets it for the batch-32 fixtures).
 # mx_h=True: a down_proj call of at most 32 rows (batched decode) takes MX rows instead -- h rounded to bf16, then
 # e4m3 with one power-of-two scale per 32 contiguous columns (engine.MX_H: the gate/up epilogue's mx_out rule,
-# csrc/common.h mx_exp), the weights per-channel as before.
+# csrc/common.h mx_exp), the weights per-channel as before.  mx_norm=True: the RMSNorm-fed linears of at most 32
+# rows (q|k|v, gate/up, the lm_head) take MX rows of the normalised input too (engine.MX_NORM: pg_norm_residual_mx
+# quantises x*(1+w) per 32-column block and the GEMV applies rstd to its outputs -- the same block-relative e4m3
+# rounding; emulated on the normalised row, so per-element bits differ where rstd is not a power of two).
 _FP8_MIN_ROWS = None
 _FP8_LM_HEAD = False
 _FP8_MX_H = False
+_FP8_MX_NORM = False
 
 
 class fp8_operands:
-    def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False):
-        self.min_rows, self.lm_head, self.mx_h = min_rows, lm_head, mx_h
+    def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False, mx_norm: bool = False):
+        self.min_rows, self.lm_head, self.mx_h, self.mx_norm = min_rows, lm_head, mx_h, mx_norm
 
     def __enter__(self):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H
-        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H)
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H = self.min_rows, self.lm_head, self.mx_h
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM
+        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM)
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM = self.min_rows, self.lm_head, self.mx_h, self.mx_norm
 
     def __exit__(self, *a):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H = self._old
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM = self._old
 
 
 def mx_exp(amax: np.ndarray) -> np.ndarray:
@@ -137,12 +141,18 @@ def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float) -> np.nd
 
 
 def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: bool = False,
-           mx: bool = False) -> np.ndarray:
-    """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation; mx: the down_proj,
-    whose <= 32-row calls take MX rows under fp8_operands(mx_h=True).)"""
+           mx: str = "") -> np.ndarray:
+    """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation; mx: "h" for the
+    down_proj, "x" for the RMSNorm-fed linears, whose <= 32-row calls take MX rows under fp8_operands(mx_h=True) /
+    (mx_norm=True).)"""
     rows = x.size // x.shape[-1]
     if gemma and _FP8_MIN_ROWS is not None and rows > _FP8_MIN_ROWS:
-        xq = mx_rows(q16(x)) if (mx and _FP8_MX_H and rows <= 32) else q8_rows(x)
+        if mx == "h" and _FP8_MX_H and rows <= 32:
+            xq = mx_rows(q16(x))
+        elif mx == "x" and _FP8_MX_NORM and rows <= 32:
+            xq = mx_rows(x)
+        else:
+            xq = q8_rows(x)
         y = xq @ q8_rows(w).T
     else:
         y = q16(x) @ w.T
@@ -280,9 +290,9 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     B, L, _ = x.shape
     nh, nkv = tcfg["num_attention_heads"], tcfg["num_key_value_heads"]
     hd = tcfg.get("head_dim", 256)
-    k = linear(x, W[lp + "k_proj.weight"], gemma=True)                              # :274
-    v = linear(x, W[lp + "v_proj.weight"], gemma=True)                              # :276
-    q = linear(x, W[lp + "q_proj.weight"], gemma=True)                              # :278
+    k = linear(x, W[lp + "k_proj.weight"], gemma=True, mx="x")                      # :274
+    v = linear(x, W[lp + "v_proj.weight"], gemma=True, mx="x")                      # :276
+    q = linear(x, W[lp + "q_proj.weight"], gemma=True, mx="x")                      # :278
     k = q16(k).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)             # :285-287
     v = q16(v).reshape(B, L, nkv, hd).transpose(0, 2, 1, 3)
     q = q16(q).reshape(B, L, nh, hd).transpose(0, 2, 1, 3)
@@ -308,9 +318,9 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
 
 def gemma_mlp(W: dict, lp: str, x: np.ndarray) -> np.ndarray:
     """GemmaMLP.forward (modeling_gemma.py:210-218)."""
-    y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"], gemma=True))
-    u = linear(x, W[lp + "up_proj.weight"], gemma=True)
-    return linear(y * u, W[lp + "down_proj.weight"], gemma=True, mx=True)
+    y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"], gemma=True, mx="x"))
+    u = linear(x, W[lp + "up_proj.weight"], gemma=True, mx="x")
+    return linear(y * u, W[lp + "down_proj.weight"], gemma=True, mx="h")
 
 
 def gemma_model(W: dict, tcfg: dict, input_embeds: np.ndarray, position_ids, mask, kv_cache,
@@ -342,7 +352,7 @@ def gemma_for_causal_lm(W: dict, tcfg: dict, input_embeds, position_ids, mask, k
     if logits_rows is not None:
         h = h[:, logits_rows]
     emb = W["language_model.model.embed_tokens.weight"]                 # tied (:492-499)
-    return linear(h, emb, W["language_model.lm_head.bias"], gemma=_FP8_LM_HEAD)   # :523-525
+    return linear(h, emb, W["language_model.lm_head.bias"], gemma=_FP8_LM_HEAD, mx="x")   # :523-525
 
 
 # --------------------------------------------------------------------------- #

@@ -191,6 +191,23 @@ __device__ __forceinline__ void scale_acc(const EpiArgs& e, int m, int n0, f32x4
   v *= (e.f.mx_in ? 1.0f : e.f.a_scale[m]) * load4_guard(e.f.w_scale, n0, e.N);   // (MX rows: scaled in the MFMA)
 }
 
+// The fp8 GEMVs' row factor: a_scale[m]; MX rows (mx_in): 1, or with ss_in (rows from pg_norm_residual_mx: x*(1+w)
+// quantised without its RMS) the RMSNorm's rstd = rsqrt(sum_i ss_in[m*ss_ld + i] / (256*ss_n) + eps)
+__device__ __forceinline__ float fp8_row_factor(const EpiArgs& e, int m) {
+  m = min(m, e.M - 1);
+  if (!e.f.mx_in) return e.f.a_scale[m];
+  if (!e.f.ss_in) return 1.0f;
+  const float* p = e.f.ss_in + (size_t)m * e.f.ss_ld;
+  float s = 0.f;
+  for (int i = 0; i < e.f.ss_n; ++i) s += p[i];
+  return rsqrtf(s / (256.0f * (float)e.f.ss_n) + e.f.eps);
+}
+// C[m][n0..n0+3] *= rf * w_scale[n0..n0+3] (rf = fp8_row_factor)
+__device__ __forceinline__ void scale_acc_rf(const EpiArgs& e, int m, int n0, f32x4& v, float rf) {
+  if (m >= e.M || n0 >= e.N) return;
+  v *= rf * load4_guard(e.f.w_scale, n0, e.N);
+}
+
 // RoPE + KV append for 4 consecutive permuted columns n0..n0+3 of row m.  The q|k|v weight rows are
 // packed so that 16-column tile t of every D-wide head block holds dims 8t..8t+7 then D/2+8t..D/2+8t+7:
 // the rotate_half partner of a lane's 4 values sits in lane ^ 32.  ALL lanes must call (shuffle).

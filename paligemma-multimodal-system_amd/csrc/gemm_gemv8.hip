@@ -114,10 +114,11 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
+    const float rf = fp8_row_factor(e, m);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       acc[t][mt] = red[0][t][mt][lane] + red[1][t][mt][lane] + red[2][t][mt][lane] + red[3][t][mt][lane];
-      scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+      scale_acc_rf(e, m, (tile0 + t) * 16 + q, acc[t][mt], rf);
     }
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
 #pragma unroll
@@ -313,8 +314,9 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
         if (m < e.M && n0 < e.N) acc[t][mt] *= sa * load4_guard(e.f.w_scale, n0, e.N);
       }
     } else {
+      const float rf = fp8_row_factor(e, m);
 #pragma unroll
-      for (int t = 0; t < NTW; ++t) scale_acc(e, m, (tile0 + t) * 16 + q, acc[t][mt]);
+      for (int t = 0; t < NTW; ++t) scale_acc_rf(e, m, (tile0 + t) * 16 + q, acc[t][mt], rf);
     }
     if constexpr (EPI == PG_EPI_BF16_GELU_MUL) {
       if (NTW == 2 && e.f.mx_out) {
@@ -414,16 +416,14 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
       return;
     }
   }
-  if constexpr (EPI == PG_EPI_F32) {
-    if (e.f.mx_in) {                               // MX rows (launch_gemv8 checked: exact, 8 or 16 chunks)
-      if (per_z == 16)
-        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
-                           e);
-      else
-        hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 8, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
-                           e);
-      return;
-    }
+  if (e.f.mx_in) {                                 // MX rows (launch_gemv8 checked: exact, 8 or 16 chunks)
+    if (per_z == 16)
+      hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
+                         e);
+    else
+      hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 8, false, true>), grid, dim3(256), lds, st, X, ldx, W, K,
+                         e);
+    return;
   }
   if (exact && per_z == 16)
     hipLaunchKernelGGL((gemv8x_kernel<EPI, NTW, MT, DEPTH, 16>), grid, dim3(256), lds, st, X, ldx, W, K, e);
@@ -454,12 +454,10 @@ static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, 
 template <int EPI, int NT>
 static void launch_gemv8_nt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
-  if constexpr (EPI == PG_EPI_F32) {
-    if (e.f.mx_in) {
-      if (e.M <= 16) launch_gemv8_mt<EPI, NT, 1, true>(X, ldx, W, K, ksplit, e, st);
-      else launch_gemv8_mt<EPI, NT, 2, true>(X, ldx, W, K, ksplit, e, st);
-      return;
-    }
+  if (e.f.mx_in) {
+    if (e.M <= 16) launch_gemv8_mt<EPI, NT, 1, true>(X, ldx, W, K, ksplit, e, st);
+    else launch_gemv8_mt<EPI, NT, 2, true>(X, ldx, W, K, ksplit, e, st);
+    return;
   }
   if (e.M <= 16)
     launch_gemv8_mt<EPI, NT, 1>(X, ldx, W, K, ksplit, e, st);

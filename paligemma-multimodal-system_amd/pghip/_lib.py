@@ -59,6 +59,7 @@ SIGNATURES = {
     "pg_synth_fill": [vp, i64, u32, f32, f32, i32, vp],
     "pg_quant_fp8": [vp, i32, i32, i32, vp, i32, vp, vp],
     "pg_norm_residual_fp8": [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, i32, i32, i32, f32, i32, vp],
+    "pg_norm_residual_mx": [vp, vp, i32, i32, vp, vp, i32, vp, vp, i32, i32, i32, i32, vp],
     "pg_xgmi_buffer_bytes": [i32, i64, C.POINTER(C.c_long)],
     "pg_xgmi_alloc": [i64, C.POINTER(C.c_void_p)],
     "pg_xgmi_free": [vp],

@@ -136,6 +136,10 @@ class PaliGemmaEngine:
     # columns (PgFusedArgs.mx_out) and the down GEMV reads those block scales into its MFMAs (mx_in) -- no
     # quantiser launch and no cross-workgroup row maximum (the block max stays inside one workgroup)
     MX_H = os.environ.get("PG_MX_H", "1") != "0"
+    # ... and the RMSNorms in front of the q|k|v, gate/up and lm_head GEMVs write MX rows of x*(1+w) with per-256-column
+    # sums of squares (pg_norm_residual_mx: one wave per 256 columns and row, no row-wide reduction); the GEMV applies
+    # rstd to its outputs.  Replaces the norm + per-row quantiser pair
+    MX_NORM = os.environ.get("PG_MX_NORM", "1") != "0"
 
     AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
     # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
@@ -360,6 +364,18 @@ class PaliGemmaEngine:
     def _fp8_rows(self, M: int) -> bool:
         return self.fp8 and M > 16
 
+    def _mx_decode(self, B: int) -> tuple:
+        """(MX h, MX norms) for a B-row decode step: the 17..32-row fp8 GEMV path with the packed fp8 weights"""
+        w = self.w
+        L0 = w.tl[0]
+        base = (self.FP8_GEMV and self._fp8_rows(B) and B <= 32 and not self.HQ_FUSED and
+                not (self.tp == 1 and self.DECODE_ADD_B32))
+        mx_h = (base and self.MX_H and "gu_w8f" in L0 and "down_w8f" in L0 and w.inter % 128 == 0
+                and w.hidden <= 4096)
+        mx_n = (mx_h and self.MX_NORM and "qkv_w8f" in L0 and w.hidden % 256 == 0
+                and getattr(w, "lm_w8f", None) is not None)
+        return mx_h, mx_n
+
     def _ksplit(self, M: int, N: int, K: int) -> int:
         """split-K of an fp32-partial GEMM (fp8 operands: the kernels count K in byte pairs).  A GEMM that will
         run as row blocks (_lin / _row_head) takes the split that suits its whole-tile head: the pt-448 x16
@@ -542,6 +558,10 @@ class PaliGemmaEngine:
         """This rank's lm_head rows [rows][vocab_local_pad] fp32 (+ bias) from normalised bf16 rows: bf16 GEMV / GEMM,
         or with fp8 weights at 17..32 rows the e4m3 rows through the fp8 GEMV (half the 1.05 GB of bf16 weights)."""
         w = self.w
+        if isinstance(xf, tuple):                   # ("mx", e4m3 rows, block scales, sums of squares)
+            _, x8, xs, ss = xf
+            return ops.gemm8(x8, None, w.lm_w8f, w.lm_s8, out, epi=ops.EPI_F32, M=rows, bias=w.lm_bias, frag=True,
+                             mx_in=xs, ss_in=ss)
         if self.FP8_GEMV and self._fp8_rows(rows) and rows <= 32 and getattr(w, "lm_w8f", None) is not None:
             H = xf.shape[1]
             x8 = self._buf(f"x8_{H}", (rows, H), torch.uint8)
@@ -641,7 +661,15 @@ class PaliGemmaEngine:
             ops.gemm_fused(None, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
             ops.gemm(h, Lw["down_w"], part, epi=ops.EPI_F32 | w.wflag, ksplit=sd)
             ns = self._allreduce_slabs(part, sd)
-        ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn, write_resid=False)
+        if B > self.FUSE_MAX_B and self._mx_decode(B)[1]:   # MX rows for the fp8 lm_head (it applies rstd)
+            H = w.hidden
+            xn = ("mx",) + ops.norm_residual_mx(res_a, w.final_w, self._buf("d_x8n", (B, H), torch.uint8),
+                                                self._buf("d_xsn", (B * H // 32,), torch.uint8),
+                                                self._buf("d_ssn", (B, H // 256), torch.float32), partials=part,
+                                                nsplit=ns, write_resid=False)
+        else:
+            ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn,
+                              write_resid=False)
         if self.tp > 1 and sampler is not None and not sampler.get("do_sample"):
             # vocabulary-parallel greedy: local (max, index) pairs -> all-reduce of the zeroed slots -> merge
             loc = self._buf("d_logits_loc", (B, w.vocab_local_pad), torch.float32)
@@ -841,24 +869,33 @@ class PaliGemmaEngine:
         hq = (self.HQ_FUSED and self.FP8_GEMV and self._fp8_rows(B) and B <= 32 and not add
               and all(k in w.tl[0] for k in ("qkv_w8f", "gu_w8f", "down_w8f"))
               and ich % self.HQ_CHUNKS == 0 and part.shape[0] >= sdh)
-        I = h.shape[1]
-        mx = (self.MX_H and not hq and not add and self.FP8_GEMV and self._fp8_rows(B) and B <= 32
-              and "gu_w8f" in w.tl[0] and "down_w8f" in w.tl[0] and I % 128 == 0 and w.hidden <= 4096)
+        I, H = h.shape[1], w.hidden
+        mx, mxn = self._mx_decode(B)
+        mx, mxn = mx and not hq and not add, mxn and not hq and not add
         if mx:
             h8 = self._buf("d_h8", (B, I), torch.uint8)
             hs = self._buf("d_hs", (B * I // 32,), torch.uint8)
+        if mxn:
+            x8n = self._buf("d_x8n", (B, H), torch.uint8)
+            xsn = self._buf("d_xsn", (B * H // 32,), torch.uint8)
+            ssn = self._buf("d_ssn", (B, H // 256), torch.float32)
         if hq:
             amax = self._buf("d_hamax", (B * self.AMAX_LD,), torch.int32)
             fa_gu = ops.fused_args(amax_out=amax, amax_ld=self.AMAX_LD)
         ns = 0
         for i, Lw in enumerate(w.tl):
-            xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
             fa = ops.fused_args(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
                                 slot_dev=st["kv_len"], slot_base=0, kc=cache.k[i], vtc=cache.vt[i], smax=cache.Smax,
                                 q_heads=nh, kv_heads=nkv, kd=cache.kd[i], vd=cache.vd[i])
-            if hq:
-                fa.amax_zero, fa.amax_zero_n = amax.data_ptr(), B * self.AMAX_LD
-            self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
+            if mxn:                                 # MX rows of x*(1+w); the q|k|v GEMV applies rstd
+                ops.norm_residual_mx(res, Lw["in_w"], x8n, xsn, ssn, partials=part, nsplit=ns)
+                ops.gemm8(x8n, None, Lw["qkv_w8f"], Lw["qkv_s8"], qb, epi=ops.EPI_QKV_ROPE, M=B, fa=fa, frag=True,
+                          mx_in=xsn, ss_in=ssn)
+            else:
+                xin = self._norm(res, Lw["in_w"], part, ns, xn, B)
+                if hq:
+                    fa.amax_zero, fa.amax_zero_n = amax.data_ptr(), B * self.AMAX_LD
+                self._lin(xin, Lw, "qkv", qb, ops.EPI_QKV_ROPE, B, fa=fa)
             a8 = self._decode_attn_merged(i, st, cache, qb, attn, part_o, part_ml, SK or self.DECODE_SPLIT_KEYS,
                                           nsplit, want_fp8=self._fp8_rows(B))
             if add:
@@ -867,6 +904,14 @@ class PaliGemmaEngine:
             else:
                 self._lin(a8 or attn, Lw, "o", part, ops.EPI_F32, B, ksplit=so)
                 n_o = self._allreduce_slabs(part, so)
+            if mxn:                                 # MX norm -> gate/up (rstd, MX h) -> down (MX rows)
+                ops.norm_residual_mx(res, Lw["post_w"], x8n, xsn, ssn, partials=part, nsplit=n_o)
+                ops.gemm8(x8n, None, Lw["gu_w8f"], Lw["gu_s8"], h8, epi=ops.EPI_BF16_GELU_MUL, M=B, frag=True,
+                          mx_in=xsn, ss_in=ssn, mx_out=hs)
+                ops.gemm8(h8, None, Lw["down_w8f"], Lw["down_s8"], part, epi=ops.EPI_F32, M=B, ksplit=sd, frag=True,
+                          mx_in=hs)
+                ns = self._allreduce_slabs(part, sd)
+                continue
             xin = self._norm(res, Lw["post_w"], part, n_o, xn, B)
             if hq:
                 self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, B, fa=fa_gu)

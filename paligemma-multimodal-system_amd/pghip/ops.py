@@ -110,12 +110,14 @@ def quant_fp8(x: torch.Tensor, q: Optional[torch.Tensor] = None, scale: Optional
 def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w_scale: torch.Tensor,
           out: torch.Tensor, *, epi: int = EPI_BF16, M: Optional[int] = None, bias: Optional[torch.Tensor] = None,
           ksplit: int = 1, fa=None, frag: bool = False, mx_in: Optional[torch.Tensor] = None,
-          mx_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+          mx_out: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None,
+          eps: float = 1e-6) -> torch.Tensor:
     """fp8 GEMM: out = epilogue((A8 . W8^T) * a_scale[m] * w_scale[n]) (PG_FP8, pg_gemm_fused).  A8, W8 are
     uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE.
     frag: W8 is fp8 fragment-packed (weights.frag_pack8) -> the weight-streaming fp8 GEMV, M <= 32.
     MX rows (frag only): mx_in = A8's E8M0 block scales [M][4][K/128] (EPI_F32; a_scale None), mx_out = the
-    scales a gelu*up launch writes beside its e4m3 h (out uint8 [M][N/2])."""
+    scales a gelu*up launch writes beside its e4m3 h (out uint8 [M][N/2]); ss_in (with mx_in, rows from
+    norm_residual_mx): the outputs are multiplied by each row's RMSNorm rstd."""
     for t, n in ((A8, "A8"), (W8, "W8")):
         if t.dtype != torch.uint8 or not t.is_cuda or t.stride(1) != 1:
             raise ValueError(f"pghip.gemm8: {n} must be a row-major uint8 (e4m3) HIP tensor")
@@ -134,6 +136,11 @@ def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w
             raise ValueError(f"pghip.gemm8: {n} must be a contiguous uint8 HIP tensor of >= {numel} E8M0 scales "
                              "(fragment-packed W8 only)")
         setattr(fa, n, t.data_ptr())
+    if ss_in is not None:
+        _chk(ss_in, torch.float32, "ss_in")
+        if mx_in is None or ss_in.stride(-1) != 1 or K % 256 or ss_in.shape[-1] < K // 256:
+            raise ValueError("pghip.gemm8: ss_in needs mx_in and fp32 [M][K/256] sums of squares")
+        fa.ss_in, fa.ss_ld, fa.ss_n, fa.eps = ss_in.data_ptr(), ss_in.stride(-2), K // 256, float(eps)
     e = epi & 0xFF
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
     if frag:
@@ -234,6 +241,26 @@ def norm_residual_fp8(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, sca
     _lib.call("pg_norm_residual_fp8", _p(resid), _p(partials), nsplit, M, _p(w), _p(b), _p(q), q.stride(-2),
               _p(scale), None, M, H, mode, float(eps), int(write_resid), _s())
     return q, scale
+
+
+def norm_residual_mx(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, qs: torch.Tensor, ss: torch.Tensor, *,
+                     partials: Optional[torch.Tensor] = None, nsplit: int = 0, write_resid: bool = True):
+    """Gemma RMSNorm feeding an MX fp8 GEMV (pg_norm_residual_mx): resid += sum of the partials' first nsplit slabs,
+    q uint8 [M][H] = e4m3 of resid*(1+w) with E8M0 block scales qs uint8 [M*H/32] ([M][4][H/128]), ss fp32 [M][H/256]
+    sums of squares; gemm8(..., mx_in=qs, ss_in=ss) applies rstd.  Returns (q, qs, ss)."""
+    _chk(resid, torch.float32, "resid")
+    _chk(w, torch.float32, "w")
+    M, H = resid.shape[-2], resid.shape[-1]
+    if (q.dtype != torch.uint8 or q.stride(-1) != 1 or q.shape[-1] < H or q.shape[0] < M or qs.dtype != torch.uint8
+            or not qs.is_contiguous() or qs.numel() < M * H // 32 or ss.dtype != torch.float32
+            or ss.stride(-1) != 1 or ss.shape[-1] < H // 256 or ss.shape[0] < M or H % 256):
+        raise ValueError("pghip.norm_residual_mx: bad output buffers (q uint8 [M][H], qs uint8 [M*H/32], "
+                         "ss fp32 [M][H/256], H % 256 == 0)")
+    if nsplit and (partials is None or partials.dtype != torch.float32):
+        raise ValueError("pghip.norm_residual_mx: fp32 partials needed for nsplit > 0")
+    _lib.call("pg_norm_residual_mx", _p(resid), _p(partials), nsplit, M, _p(w), _p(q), q.stride(-2), _p(qs), _p(ss),
+              ss.stride(-2), M, H, int(write_resid), _s())
+    return q, qs, ss
 
 
 def attention(q, q_rs, o, o_rs, k, k_bs, k_hs, k_rs, vt, vt_bs, vt_hs, vt_ds, *, B, Lq, Lkv, Hq, Hkv, D,

@@ -1,7 +1,7 @@
 """Operand-rounding emulation fixtures from the numpy ORACLE (not the reference): the fp32 oracle run with the HIP
 fp8 path's operand rounding -- bf16 operands everywhere, e4m3 Gemma linears and tied lm_head with per-row /
 per-channel scales (oracle.paligemma_oracle.fp8_operands; min_rows=0: prefill and batch > 16 decode both run fp8;
-mx_h=True: the decode down_proj on MX rows, engine.MX_H) -- on a reference
+mx_h / mx_norm: the decode down_proj and the RMSNorm-fed decode linears on MX rows, engine.MX_H / MX_NORM) -- on a reference
 golden's requests, teacher-forced with the reference's own greedy ids.  Stored per image and step: the emulated
 logits at the reference's top-64 ids, the emulated argmax and top1-top2 margin.  tests/test_large_gpu.py bounds the
 HIP fp8 path's distance to the reference by 1.5x this intrinsic distance (the bf16 tests do the same with
@@ -40,7 +40,8 @@ def make(name: str, cfg: dict):
     W = synth.generate_state_dict(cfg, gain)
     size = cfg["vision_config"]["image_size"]
     out = {"linear_gain": np.float32(gain),
-           "mode": np.array("bf16 operands + e4m3 Gemma linears and lm_head (min_rows=0), MX decode down_proj rows")}
+           "mode": np.array("bf16 operands + e4m3 Gemma linears and lm_head (min_rows=0), MX decode rows (down_proj h, "
+                                   "RMSNorm-fed q|k|v, gate/up, lm_head)")}
     for j, seed in enumerate(g["seeds"]):
         p = f"i{j}_"
         pv = pixels(int(seed), size)
@@ -54,7 +55,7 @@ def make(name: str, cfg: dict):
         mask = np.ones_like(ids)
         cur = ids
         vals, am, mg = [], [], []
-        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True):
+        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True, mx_norm=True):
             for t in range(steps):
                 lg = orc.forward(cur, pv, mask, kv, logits_rows=slice(-1, None))["logits"][0, -1]
                 vals.append(lg[top_ids[t]])

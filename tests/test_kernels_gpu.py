@@ -1025,6 +1025,54 @@ def test_mx_h_gate_up_and_down(M, I, H, ks):
         assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
 
 
+@pytest.mark.parametrize("M,H,nsplit,I", [(32, 2048, 8, 16384), (17, 2048, 2, 4096), (24, 512, 0, 1024),
+                                          (32, 2048, 11, 2048)])
+def test_mx_norm_rows_and_rstd_consumers(M, H, nsplit, I):
+    """pg_norm_residual_mx (ABI 11, engine.MX_NORM): the residual update equals resid + the slabs in slab order
+    (bitwise), the e4m3 rows and E8M0 block scales equal the torch MX rule on x*(1+w) (bitwise), the per-256-column
+    sums of squares match; an fp8 GEMV fed those rows (mx_in + ss_in) equals rstd * the fp32 matmul of the dequantised
+    rows -- the RMSNorm split at rstd -- for the fp32 slab and the gelu*up (with MX h out) epilogues."""
+    from pghip import ops
+    from pghip.weights import frag_pack8, quant_rows_fp8
+    g = torch.Generator().manual_seed(95)
+    resid = (torch.randn(M, H, generator=g) * 3).cuda()
+    part = (torch.randn(max(nsplit, 1), M, H, generator=g) * 0.5).cuda()
+    w = (torch.randn(H, generator=g) * 0.2).cuda()
+    want = resid.clone()
+    for s in range(nsplit):
+        want += part[s]
+    r = resid.clone()
+    q = torch.empty(M, H, dtype=torch.uint8, device="cuda")
+    qs = torch.empty(M * H // 32, dtype=torch.uint8, device="cuda")
+    ss = torch.empty(M, H // 256, device="cuda")
+    ops.norm_residual_mx(r, w, q, qs, ss, partials=part, nsplit=nsplit)
+    assert torch.equal(r, want)
+    q_ref, s_ref = _mx_quant(want * (1 + w))
+    assert torch.equal(qs, s_ref)
+    assert torch.equal(q, q_ref)
+    assert torch.allclose(ss, want.view(M, H // 256, 256).pow(2).sum(-1), rtol=1e-5, atol=0)
+    r2 = resid.clone()
+    ops.norm_residual_mx(r2, w, q, qs, ss, partials=part, nsplit=nsplit, write_resid=False)
+    assert torch.equal(r2, resid)
+    rstd = torch.rsqrt(want.double().pow(2).mean(-1, keepdim=True) + 1e-6)
+    xd = _mx_deq(q, qs, M, H).double()
+    Wd = rnd(H, H, scale=1 / math.sqrt(H), seed=96)
+    d8, ds = quant_rows_fp8(Wd)
+    out = torch.empty(2, M, H, device="cuda")
+    ops.gemm8(q, None, frag_pack8(d8), ds, out, epi=ops.EPI_F32, M=M, ksplit=2, frag=True, mx_in=qs, ss_in=ss)
+    ref = (rstd * (xd @ _deq(d8, ds).double().t())).float()
+    assert err(out.sum(0), ref) < 1e-4, float(err(out.sum(0), ref))
+    Wgu = rnd(2 * I, H, scale=1 / math.sqrt(H), seed=97)
+    gu8, gus = quant_rows_fp8(Wgu)
+    h8 = torch.empty(M, I, dtype=torch.uint8, device="cuda")
+    hs = torch.empty(M * I // 32, dtype=torch.uint8, device="cuda")
+    ops.gemm8(q, None, frag_pack8(gu8), gus, h8, epi=ops.EPI_BF16_GELU_MUL, M=M, frag=True, mx_in=qs, ss_in=ss,
+              mx_out=hs)
+    gg = (rstd * (xd @ _deq(gu8, gus).double().t())).float().view(M, I // 16, 2, 16)
+    hw = (torch.nn.functional.gelu(gg[:, :, 0], approximate="tanh") * gg[:, :, 1]).reshape(M, I)
+    assert err(_mx_deq(h8, hs, M, I), hw) < 0.07                # e4m3 h per 32-column block
+
+
 @pytest.mark.parametrize("M,N,K,ks", [(16, 2048, 16384, 8), (16, 2048, 2048, 2), (8, 1024, 4096, 4), (16, 512, 1024, 1)])
 def test_gemv_fin_residual_xprime_and_pair_sums(M, N, K, ks):
     """PG_EPI_F32_FIN on the bf16 GEMV (5..16-row decode): the residual += x.W^T (+ bias) finalised in-kernel, x' =
