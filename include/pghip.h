@@ -120,7 +120,8 @@ typedef struct PgFusedArgs {
   const uint8_t* mx_in;     /* PG_FP8|PG_W_FRAG (any epilogue but F32_ADD), M <= 32, pro_mode 0: A is e4m3 [M][lda]
                                with mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale
                                is not read.  With ss_in (rows from pg_norm_residual_mx, ss_n = K/256, eps) the outputs
-                               are multiplied by the row's rstd = rsqrt(sum ss_in[m*ss_ld + i] / K + eps)            */
+                               are multiplied by the row's rstd = rsqrt(sum ss_in[m*ss_ld + i] / K + eps), ss_n =
+                               K / 1024 <= 4                                                                        */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -264,9 +265,9 @@ int pg_norm_residual_fp8(float* resid, const float* partials, int nsplit, int M_
                          int H, int mode, float eps, int write_resid, hipStream_t stream);
 /* (ABI 11) Gemma RMSNorm for MX fp8 consumers (GemmaRMSNorm modeling_gemma.py:165-182 split at rstd): x = resid +
  * sum_s partials[s] (slab order; written back when write_resid), q uint8 [M][ldq] = e4m3 of y = x*(1+w) with one
- * E8M0 scale per 32 columns in qs [M][4][H/128] (the PgFusedArgs.mx_out rule), ss [M][ss_ld] = sum of x^2 per 256
- * columns.  The consumer (an fp8 GEMV with mx_in = qs, ss_in = ss, ss_n = H/256, eps) applies rstd to its outputs.
- * H % 256 == 0; resid, partials, w 16-B aligned. */
+ * E8M0 scale per 32 columns in qs [M][4][H/128] (the PgFusedArgs.mx_out rule), ss [M][ss_ld] = sum of x^2 per 1024
+ * columns.  The consumer (an fp8 GEMV with mx_in = qs, ss_in = ss, ss_n = H/1024, eps) applies rstd to its outputs.
+ * H % 1024 == 0; resid, partials, w 16-B aligned. */
 int pg_norm_residual_mx(float* resid, const float* partials, int nsplit, int M_part, const float* w, void* q,
                         int ldq, void* qs, float* ss, int ss_ld, int M, int H, int write_resid, hipStream_t stream);
 

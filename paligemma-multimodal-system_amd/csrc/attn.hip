@@ -733,16 +733,6 @@ __global__ __launch_bounds__(256) void attn_lds_kernel(AttnArgs a) {
 // skipped when no row's max moved), and 2 x DT PV MFMAs.  Keys past Lkv: K rows clamped, scores -inf,
 // V^T chunks clamped to the last readable 8-key chunk (rup8(Lkv) keys must be readable per V^T row);
 // K dims past D (D < DP) are never read from memory.
-// prefill key splits: at most PF_MAXS per row; PG_PF_MERGE 1 merges them inside attn_fa_kernel (ticket per (batch,
-// kv head, row tile) in pg_pf_cnt: zero at module load, self-resetting -- one split prefill attention in flight per
-// process), 0 in a separate attn_pf_combine_kernel launch
-#define PF_MAXS 8
-#ifndef PG_PF_MERGE
-#define PG_PF_MERGE 1
-#endif
-#define PF_CNT_MAX 16384
-static __device__ int pg_pf_cnt[PF_CNT_MAX];
-
 template <int DP, int DT, int WAVES, int RPW, int KB = 64, int NST = 2>
 __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   static_assert(KB == 64 || KB == 32, "64- or 32-key blocks");
@@ -919,62 +909,16 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     }
   }
   if (nks > 1) {
-    // unnormalised O and the row's (m, l) of this key split, stored write-through (sc1) for the merge below
-    const long pb = ((long)b * a.Hkv + kvh) * nks * R;           // (b, kv head)'s first partial row
-    const __amdgpu_buffer_rsrc_t ro = pg_rsrc(a.part_o + pb * (DT * 16));
+    // unnormalised O and the row's (m, l) of this key split
 #pragma unroll
     for (int i = 0; i < RPW; ++i) {
       if (!rvalid[i]) continue;
-      const int row = ks * R + rrow[i];
+      const long prow = (((long)b * a.Hkv + kvh) * nks + ks) * R + rrow[i];
+      float* po = a.part_o + prow * (DT * 16);
 #pragma unroll
-      for (int tt = 0; tt < DT; ++tt) st16_sc1(ro, (row * (DT * 16) + 16 * tt + 4 * g) * 4, o[i][tt]);
-      if (g == 0)
-        __hip_atomic_store((pg_gu64*)(a.part_ml + (pb + row) * 2), __builtin_bit_cast(unsigned long long,
-                           f32x2{m[i], l[i]}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int tt = 0; tt < DT; ++tt) *(f32x4*)(po + 16 * tt + 4 * g) = o[i][tt];
+      if (g == 0) *(f32x2*)(a.part_ml + prow * 2) = f32x2{m[i], l[i]};
     }
-    if (!PG_PF_MERGE) return;                      // (the host launches attn_pf_combine_kernel)
-    // one agent-scope ticket per (batch, kv head, row tile): the workgroup of the last-arriving split merges the
-    // nks partials of the tile's rows (sc1 loads, as attn_decode_fused_kernel) -- no combine launch
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* s_last = (int*)smem;                      // (the ring is idle: every wave has passed the barrier above)
-    int* cnt = pg_pf_cnt + ((long)b * a.Hkv + kvh) * ((int)gridDim.x / nks) + rt;
-    if (t == 0) *s_last = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nks - 1;
-    __syncthreads();
-    if (!*s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");      // compiler-only: the loads stay below the ticket
-    const int r0 = rt * WAVES * RPW * 16, nr = min(WAVES * RPW * 16, R - r0), D4 = D >> 2;
-    for (int it = t; it < nr * D4; it += WAVES * 64) {
-      const int r = r0 + it / D4, d4 = it % D4;
-      f32x2 ml[PF_MAXS];
-      f32x4 ov[PF_MAXS];
-#pragma unroll
-      for (int s2 = 0; s2 < PF_MAXS; ++s2) {
-        const int srow = min(s2, nks - 1) * R + r;
-        ml[s2] = ld8_wt(a.part_ml + (pb + srow) * 2);
-        ov[s2] = ld16_sc1(ro, (srow * (DT * 16) + 4 * d4) * 4);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      float M = -INFINITY;
-#pragma unroll
-      for (int s2 = 0; s2 < PF_MAXS; ++s2)
-        if (s2 < nks) M = fmaxf(M, ml[s2][0]);
-      float den = 0.f;
-      f32x4 num = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < PF_MAXS; ++s2) {
-        const float w = (s2 < nks && ml[s2][0] != -INFINITY) ? exp2f(ml[s2][0] - M) : 0.f;
-        den += w * ml[s2][1];
-        num += w * ov[s2];
-      }
-      const float inv = 1.0f / den;
-      const int rp = r / a.G, rh = kvh * a.G + r % a.G;
-      u32x2 pk;
-      pk[0] = pack_bf2(num[0] * inv, num[1] * inv);
-      pk[1] = pack_bf2(num[2] * inv, num[3] * inv);
-      *(u32x2*)(a.o + ((long)b * a.Lq + rp) * a.o_rs + (long)rh * D + 4 * d4) = pk;
-    }
-    if (t == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
 #pragma unroll
@@ -1066,6 +1010,7 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(const float* __restri
 
 // Merge the key-split prefill partials: o[b][pos][hq][d] = sum_s 2^(m_s - M) O_s / sum_s 2^(m_s - M) l_s, one thread
 // per (row, 4 dims), every split's (m, l, O) loaded before the first is used.
+#define PF_MAXS 8
 __global__ __launch_bounds__(256) void attn_pf_combine_kernel(const float* __restrict__ part_o,
                                                               const float* __restrict__ part_ml, int nks, int R, int G,
                                                               int Hkv, int D, int DW, int Lq, bf16_t* __restrict__ o,
@@ -1241,9 +1186,6 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
     if (nsplit > 1) {
       // prefill key split (caller's workspace: part_o [B][Hkv][nsplit][Lq*G][DT*16] fp32, part_ml [..][2])
       PG_REQUIRE(nsplit <= PF_MAXS && part_o && part_ml && D % 4 == 0);
-      // (the in-kernel merge: one ticket per (batch, kv head, row tile); sc1 offsets of a (batch, kv head) in 31 bits)
-      PG_REQUIRE(!PG_PF_MERGE || ((long)B * Hkv * grid.x <= PF_CNT_MAX &&
-                                  (long)nsplit * Lq * G * DT * 16 * 4 < (1l << 31)));
       a.pf_splits = nsplit;
       grid.x *= nsplit;
     }
@@ -1273,7 +1215,7 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
   ATTN_DISPATCH(256, 16)   // Gemma head_dim 256
   if (!launched) return (int)hipErrorInvalidValue;
   PG_LAUNCH_CHECK();
-  if (a.pf_splits > 1 && !PG_PF_MERGE) {
+  if (a.pf_splits > 1) {
     const long total = (long)B * Hkv * Lq * G * (D / 4);
     hipLaunchKernelGGL(attn_pf_combine_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, part_o,
                        part_ml, nsplit, Lq * G, G, Hkv, D, DT * 16, Lq, (bf16_t*)o, o_rs, total);

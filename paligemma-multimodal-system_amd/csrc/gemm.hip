@@ -53,9 +53,13 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (epi == PG_EPI_FX_ADD) PG_REQUIRE(M <= 16 && !fp8 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N &&
                                        ((uintptr_t)C & 15) == 0 && ldc % 2 == 0);
   if (f.mx_in) PG_REQUIRE(fp8 && frag && epi != PG_EPI_F32_ADD && M <= 32 && f.pro_mode == 0 && K % 128 == 0 &&
-                          A != nullptr && (!f.ss_in || (f.ss_n > 0 && f.ss_ld >= f.ss_n && K == 256 * f.ss_n)));
-  if (f.mx_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.pro_mode == 0 && !f.amax_out && ksplit == 1 &&
-                           (N / 2) % 128 == 0 && PG_GEMV8_WIDE && ((K >> 7) + ksplit - 1) / ksplit * 128 <= 4096);
+                          A != nullptr && ((uintptr_t)f.mx_in & 15) == 0 &&
+                          (!f.ss_in || (f.ss_n > 0 && f.ss_n <= 4 && f.ss_ld >= f.ss_n && K == 1024 * f.ss_n)));
+  // mx_out is written by the wide form only (gemv8x_kernel, NTW 2): launch_gemv8 takes it for GELU_MUL whenever a
+  // split's x fits the LDS -- and, with MX rows in, when the split's chunk count is a compile-time 8 or 16
+  if (f.mx_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.pro_mode == 0 && !f.amax_out &&
+                           ksplit == 1 && (N / 2) % 128 == 0 && PG_GEMV8_WIDE && (K >> 7) * 128 <= 4096 &&
+                           (!f.mx_in || (K >> 7) == 8 || (K >> 7) == 16));
   if (f.fx) PG_REQUIRE(((uintptr_t)f.fx & 15) == 0 && (f.pro_mode == 1) != (epi == PG_EPI_F32_FIN) && !fp8 &&
                        M <= 16);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD || epi == PG_EPI_FX_ADD);

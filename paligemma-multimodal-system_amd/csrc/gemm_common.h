@@ -192,16 +192,33 @@ __device__ __forceinline__ void scale_acc(const EpiArgs& e, int m, int n0, f32x4
 }
 
 // The fp8 GEMVs' row factor: a_scale[m]; MX rows (mx_in): 1, or with ss_in (rows from pg_norm_residual_mx: x*(1+w)
-// quantised without its RMS) the RMSNorm's rstd = rsqrt(sum_i ss_in[m*ss_ld + i] / (256*ss_n) + eps)
-__device__ __forceinline__ float fp8_row_factor(const EpiArgs& e, int m) {
+// quantised without its RMS) the RMSNorm's rstd = rsqrt(sum_i ss_in[m*ss_ld + i] / (1024*ss_n) + eps)
+// Two halves so a kernel can issue the loads ahead of its weight stream and reduce them in the epilogue: every load
+// is issued before any is used (ss_n <= 4, host-checked), one memory round trip
+struct Fp8RowLoads {
+  float v[4];
+};
+__device__ __forceinline__ Fp8RowLoads fp8_row_load(const EpiArgs& e, int m) {
+  Fp8RowLoads r;
   m = min(m, e.M - 1);
-  if (!e.f.mx_in) return e.f.a_scale[m];
-  if (!e.f.ss_in) return 1.0f;
-  const float* p = e.f.ss_in + (size_t)m * e.f.ss_ld;
-  float s = 0.f;
-  for (int i = 0; i < e.f.ss_n; ++i) s += p[i];
-  return rsqrtf(s / (256.0f * (float)e.f.ss_n) + e.f.eps);
+  if (!e.f.mx_in) {
+    r.v[0] = e.f.a_scale[m];
+  } else if (e.f.ss_in) {
+    const float* p = e.f.ss_in + (size_t)m * e.f.ss_ld;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.v[i] = p[min(i, e.f.ss_n - 1)];
+  }
+  return r;
 }
+__device__ __forceinline__ float fp8_row_finish(const EpiArgs& e, const Fp8RowLoads& r) {
+  if (!e.f.mx_in) return r.v[0];
+  if (!e.f.ss_in) return 1.0f;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += i < e.f.ss_n ? r.v[i] : 0.f;
+  return rsqrtf(s / (1024.0f * (float)e.f.ss_n) + e.f.eps);
+}
+__device__ __forceinline__ float fp8_row_factor(const EpiArgs& e, int m) { return fp8_row_finish(e, fp8_row_load(e, m)); }
 // C[m][n0..n0+3] *= rf * w_scale[n0..n0+3] (rf = fp8_row_factor)
 __device__ __forceinline__ void scale_acc_rf(const EpiArgs& e, int m, int n0, f32x4& v, float rf) {
   if (m >= e.M || n0 >= e.N) return;

@@ -49,6 +49,10 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
     mxr[mt] = MX ? e.f.mx_in + (size_t)min(mt * 16 + r, M - 1) * (K >> 5) + (size_t)g * nch_all : nullptr;
+  // the epilogue's row factors (a_scale, or the MX rows' sums of squares) issued ahead of the weight stream
+  Fp8RowLoads rl[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) rl[mt] = fp8_row_load(e, mt * 16 + r);
   auto load = [&](int j, u32x4 (&wv)[NT][2], u32x4 (&xv)[MT][2], int (&sv)[MT]) {
     const size_t cc = (size_t)(c0 + wave + j * 4);
     if constexpr (MX) {
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
     const int m = mt * 16 + r;
-    const float rf = fp8_row_factor(e, m);
+    const float rf = fp8_row_finish(e, rl[mt]);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       acc[t][mt] = red[0][t][mt][lane] + red[1][t][mt][lane] + red[2][t][mt][lane] + red[3][t][mt][lane];
@@ -196,14 +200,27 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
   }
   // MX rows: this lane's E8M0 scale of block g of each of its CPW chunks, rows r and 16 + r (loaded with the x pieces,
   // before the W stream; the step-3 wait covers them)
-  int sbx[MX ? MT : 1][MX ? CPW : 1];
+  // (the CPW bytes are consecutive and CPW-aligned: one 8- or 16-byte load per row tile)
+  u32x4 sbv[MX ? MT : 1];
   if constexpr (MX) {
+    static_assert(CPW == 8 || CPW == 16, "MX scale bytes load as one 8- or 16-byte vector");
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const uint8_t* sp = e.f.mx_in + (size_t)min(mt * 16 + r, M - 1) * (K >> 5) + (size_t)g * nch_all + c0;
-#pragma unroll
-      for (int j = 0; j < CPW; ++j) sbx[mt][j] = sp[j];
+      if constexpr (CPW == 16) {
+        sbv[mt] = *(const u32x4*)sp;
+      } else {
+        const u32x2 h = *(const u32x2*)sp;
+        sbv[mt] = u32x4{h[0], h[1], 0u, 0u};
+      }
     }
+  }
+  auto sbx = [&](int mt, int j) -> int { return (int)((sbv[mt][j >> 2] >> (8 * (j & 3))) & 0xffu); };
+  // the epilogue's row factors, issued with the x pieces (not with XB: its scale comes from amax_in)
+  Fp8RowLoads rl[XB ? 1 : MT];
+  if constexpr (!XB) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) rl[mt] = fp8_row_load(e, mt * 16 + r);
   }
   // the x DMA pieces stay ahead of every W load in the vmcnt order (step 3 waits for "at most the W loads
   // outstanding"): the scheduler may not hoist a W load above them
@@ -269,7 +286,7 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
       for (int mt = 0; mt < MT; ++mt) {
         if constexpr (MX)
           acc[t][mt] = mfma8s(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
-                              xf[mt][1], acc[t][mt], sbx[mt][MX ? j : 0]);
+                              xf[mt][1], acc[t][mt], sbx(mt, j));
         else
           acc[t][mt] = mfma8(__builtin_bit_cast(bf16x8, wv[t][0]), __builtin_bit_cast(bf16x8, wv[t][1]), xf[mt][0],
                              xf[mt][1], acc[t][mt]);
@@ -314,7 +331,7 @@ __global__ __launch_bounds__(256) void gemv8x_kernel(const uint8_t* __restrict__
         if (m < e.M && n0 < e.N) acc[t][mt] *= sa * load4_guard(e.f.w_scale, n0, e.N);
       }
     } else {
-      const float rf = fp8_row_factor(e, m);
+      const float rf = fp8_row_finish(e, rl[mt]);
 #pragma unroll
       for (int t = 0; t < NTW; ++t) scale_acc_rf(e, m, (tile0 + t) * 16 + q, acc[t][mt], rf);
     }

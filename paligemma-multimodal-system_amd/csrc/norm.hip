@@ -209,13 +209,13 @@ extern "C" int pg_norm_residual_fp8(float* resid, const float* partials, int nsp
 // Gemma RMSNorm for MX fp8 consumers (17..32-row fp8 decode, engine.MX_NORM): x = resid + sum_s partials[s] (slab
 // order; written back when write_resid), y = x * (1 + w) as e4m3 bytes q [M][ldq] with one E8M0 scale per 32
 // columns (qs [M][4][H/128], the PgFusedArgs.mx_out rule and layout), and ss [M][ss_ld] the sum of x^2 over each
-// 256 columns.  The row's rstd is left to the consumer (PgFusedArgs.mx_in + ss_in): no row-wide reduction here, so
-// every (256 columns, row) is its own one-wave workgroup -- H/256 x M workgroups, one memory round trip.
-__global__ __launch_bounds__(64) void norm_mx_kernel(float* __restrict__ resid, const float* __restrict__ partials,
-                                                     int nsplit, int M_part, const float* __restrict__ w,
-                                                     uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ qs,
-                                                     float* __restrict__ ss, int ss_ld, int H, int write_resid) {
-  const int t = threadIdx.x, m = blockIdx.y, c = blockIdx.x * 256 + 4 * t;
+// 1024 columns.  The row's rstd is left to the consumer (PgFusedArgs.mx_in + ss_in): no row-wide reduction here, so
+// every (1024 columns, row) is its own workgroup -- H/1024 x M workgroups, one memory round trip.
+__global__ __launch_bounds__(256) void norm_mx_kernel(float* __restrict__ resid, const float* __restrict__ partials,
+                                                      int nsplit, int M_part, const float* __restrict__ w,
+                                                      uint8_t* __restrict__ q, int ldq, uint8_t* __restrict__ qs,
+                                                      float* __restrict__ ss, int ss_ld, int H, int write_resid) {
+  const int t = threadIdx.x, m = blockIdx.y, c = blockIdx.x * 1024 + 4 * t;
   const size_t o = (size_t)m * H + c;
   f32x4 x = *(const f32x4*)(resid + o);
   const f32x4 wv = *(const f32x4*)(w + c);
@@ -246,18 +246,21 @@ __global__ __launch_bounds__(64) void norm_mx_kernel(float* __restrict__ resid, 
     const int kb = c >> 5;
     qs[(size_t)m * (H >> 5) + (size_t)(kb & 3) * (H >> 7) + (kb >> 2)] = (uint8_t)(ex + 127);
   }
+  __shared__ float sw[4];
   const float s2 = wave_sum(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
-  if (t == 0) ss[(size_t)m * ss_ld + blockIdx.x] = s2;
+  if ((t & 63) == 0) sw[t >> 6] = s2;
+  __syncthreads();
+  if (t == 0) ss[(size_t)m * ss_ld + blockIdx.x] = (sw[0] + sw[1]) + (sw[2] + sw[3]);
 }
 
 extern "C" int pg_norm_residual_mx(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                                    void* q, int ldq, void* qs, float* ss, int ss_ld, int M, int H, int write_resid,
                                    hipStream_t stream) {
-  PG_REQUIRE(M > 0 && M <= M_part && H > 0 && H % 256 == 0 && q && qs && ss && ldq >= H && ldq % 4 == 0 &&
-             ss_ld >= H / 256 && nsplit >= 0 && (nsplit == 0 || partials));
+  PG_REQUIRE(M > 0 && M <= M_part && H > 0 && H % 1024 == 0 && q && qs && ss && ldq >= H && ldq % 4 == 0 &&
+             ss_ld >= H / 1024 && nsplit >= 0 && (nsplit == 0 || partials));
   PG_REQUIRE(((uintptr_t)resid & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)q & 3) == 0 &&
              ((uintptr_t)partials & 15) == 0);
-  hipLaunchKernelGGL(norm_mx_kernel, dim3(H / 256, M), dim3(64), 0, stream, resid, partials, nsplit, M_part, w,
+  hipLaunchKernelGGL(norm_mx_kernel, dim3(H / 1024, M), dim3(256), 0, stream, resid, partials, nsplit, M_part, w,
                      (uint8_t*)q, ldq, (uint8_t*)qs, ss, ss_ld, H, write_resid);
   PG_LAUNCH_CHECK();
   return 0;

@@ -136,8 +136,8 @@ class PaliGemmaEngine:
     # columns (PgFusedArgs.mx_out) and the down GEMV reads those block scales into its MFMAs (mx_in) -- no
     # quantiser launch and no cross-workgroup row maximum (the block max stays inside one workgroup)
     MX_H = os.environ.get("PG_MX_H", "1") != "0"
-    # ... and the RMSNorms in front of the q|k|v, gate/up and lm_head GEMVs write MX rows of x*(1+w) with per-256-column
-    # sums of squares (pg_norm_residual_mx: one wave per 256 columns and row, no row-wide reduction); the GEMV applies
+    # ... and the RMSNorms in front of the q|k|v, gate/up and lm_head GEMVs write MX rows of x*(1+w) with per-1024-column
+    # sums of squares (pg_norm_residual_mx: one workgroup per 1024 columns and row, no row-wide reduction); the GEMV applies
     # rstd to its outputs.  Replaces the norm + per-row quantiser pair
     MX_NORM = os.environ.get("PG_MX_NORM", "1") != "0"
 
@@ -372,7 +372,7 @@ class PaliGemmaEngine:
                 not (self.tp == 1 and self.DECODE_ADD_B32))
         mx_h = (base and self.MX_H and "gu_w8f" in L0 and "down_w8f" in L0 and w.inter % 128 == 0
                 and w.hidden <= 4096)
-        mx_n = (mx_h and self.MX_NORM and "qkv_w8f" in L0 and w.hidden % 256 == 0
+        mx_n = (mx_h and self.MX_NORM and "qkv_w8f" in L0 and w.hidden % 1024 == 0
                 and getattr(w, "lm_w8f", None) is not None)
         return mx_h, mx_n
 
@@ -665,7 +665,7 @@ class PaliGemmaEngine:
             H = w.hidden
             xn = ("mx",) + ops.norm_residual_mx(res_a, w.final_w, self._buf("d_x8n", (B, H), torch.uint8),
                                                 self._buf("d_xsn", (B * H // 32,), torch.uint8),
-                                                self._buf("d_ssn", (B, H // 256), torch.float32), partials=part,
+                                                self._buf("d_ssn", (B, H // 1024), torch.float32), partials=part,
                                                 nsplit=ns, write_resid=False)
         else:
             ops.norm_residual(res_a, w.final_w, mode=ops.NORM_RMS, partials=part, nsplit=ns, out=xn,
@@ -878,7 +878,7 @@ class PaliGemmaEngine:
         if mxn:
             x8n = self._buf("d_x8n", (B, H), torch.uint8)
             xsn = self._buf("d_xsn", (B * H // 32,), torch.uint8)
-            ssn = self._buf("d_ssn", (B, H // 256), torch.float32)
+            ssn = self._buf("d_ssn", (B, H // 1024), torch.float32)
         if hq:
             amax = self._buf("d_hamax", (B * self.AMAX_LD,), torch.int32)
             fa_gu = ops.fused_args(amax_out=amax, amax_ld=self.AMAX_LD)

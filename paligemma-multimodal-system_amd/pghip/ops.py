@@ -138,9 +138,9 @@ def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w
         setattr(fa, n, t.data_ptr())
     if ss_in is not None:
         _chk(ss_in, torch.float32, "ss_in")
-        if mx_in is None or ss_in.stride(-1) != 1 or K % 256 or ss_in.shape[-1] < K // 256:
-            raise ValueError("pghip.gemm8: ss_in needs mx_in and fp32 [M][K/256] sums of squares")
-        fa.ss_in, fa.ss_ld, fa.ss_n, fa.eps = ss_in.data_ptr(), ss_in.stride(-2), K // 256, float(eps)
+        if mx_in is None or ss_in.stride(-1) != 1 or K % 1024 or not 0 < K // 1024 <= 4 or ss_in.shape[-1] < K // 1024:
+            raise ValueError("pghip.gemm8: ss_in needs mx_in and fp32 [M][K/1024] sums of squares (K <= 4096)")
+        fa.ss_in, fa.ss_ld, fa.ss_n, fa.eps = ss_in.data_ptr(), ss_in.stride(-2), K // 1024, float(eps)
     e = epi & 0xFF
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
     if frag:
@@ -246,16 +246,16 @@ def norm_residual_fp8(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, sca
 def norm_residual_mx(resid: torch.Tensor, w: torch.Tensor, q: torch.Tensor, qs: torch.Tensor, ss: torch.Tensor, *,
                      partials: Optional[torch.Tensor] = None, nsplit: int = 0, write_resid: bool = True):
     """Gemma RMSNorm feeding an MX fp8 GEMV (pg_norm_residual_mx): resid += sum of the partials' first nsplit slabs,
-    q uint8 [M][H] = e4m3 of resid*(1+w) with E8M0 block scales qs uint8 [M*H/32] ([M][4][H/128]), ss fp32 [M][H/256]
-    sums of squares; gemm8(..., mx_in=qs, ss_in=ss) applies rstd.  Returns (q, qs, ss)."""
+    q uint8 [M][H] = e4m3 of resid*(1+w) with E8M0 block scales qs uint8 [M*H/32] ([M][4][H/128]), ss fp32
+    [M][H/1024] sums of squares; gemm8(..., mx_in=qs, ss_in=ss) applies rstd.  Returns (q, qs, ss)."""
     _chk(resid, torch.float32, "resid")
     _chk(w, torch.float32, "w")
     M, H = resid.shape[-2], resid.shape[-1]
     if (q.dtype != torch.uint8 or q.stride(-1) != 1 or q.shape[-1] < H or q.shape[0] < M or qs.dtype != torch.uint8
             or not qs.is_contiguous() or qs.numel() < M * H // 32 or ss.dtype != torch.float32
-            or ss.stride(-1) != 1 or ss.shape[-1] < H // 256 or ss.shape[0] < M or H % 256):
+            or ss.stride(-1) != 1 or ss.shape[-1] < H // 1024 or ss.shape[0] < M or H % 1024):
         raise ValueError("pghip.norm_residual_mx: bad output buffers (q uint8 [M][H], qs uint8 [M*H/32], "
-                         "ss fp32 [M][H/256], H % 256 == 0)")
+                         "ss fp32 [M][H/1024], H % 1024 == 0)")
     if nsplit and (partials is None or partials.dtype != torch.float32):
         raise ValueError("pghip.norm_residual_mx: fp32 partials needed for nsplit > 0")
     _lib.call("pg_norm_residual_mx", _p(resid), _p(partials), nsplit, M, _p(w), _p(q), q.stride(-2), _p(qs), _p(ss),

@@ -1025,12 +1025,12 @@ def test_mx_h_gate_up_and_down(M, I, H, ks):
         assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
 
 
-@pytest.mark.parametrize("M,H,nsplit,I", [(32, 2048, 8, 16384), (17, 2048, 2, 4096), (24, 512, 0, 1024),
-                                          (32, 2048, 11, 2048)])
+@pytest.mark.parametrize("M,H,nsplit,I", [(32, 2048, 8, 16384), (17, 2048, 2, 4096), (24, 3072, 0, 1024),
+                                          (32, 2048, 11, 2048), (20, 1024, 1, 2048)])
 def test_mx_norm_rows_and_rstd_consumers(M, H, nsplit, I):
     """pg_norm_residual_mx (ABI 11, engine.MX_NORM): the residual update equals resid + the slabs in slab order
     (bitwise), the e4m3 rows and E8M0 block scales equal the torch MX rule on x*(1+w) (bitwise), the per-256-column
-    sums of squares match; an fp8 GEMV fed those rows (mx_in + ss_in) equals rstd * the fp32 matmul of the dequantised
+    sums of squares (per 1024 columns) match; an fp8 GEMV fed those rows (mx_in + ss_in) equals rstd * the fp32 matmul of the dequantised
     rows -- the RMSNorm split at rstd -- for the fp32 slab and the gelu*up (with MX h out) epilogues."""
     from pghip import ops
     from pghip.weights import frag_pack8, quant_rows_fp8
@@ -1044,13 +1044,13 @@ def test_mx_norm_rows_and_rstd_consumers(M, H, nsplit, I):
     r = resid.clone()
     q = torch.empty(M, H, dtype=torch.uint8, device="cuda")
     qs = torch.empty(M * H // 32, dtype=torch.uint8, device="cuda")
-    ss = torch.empty(M, H // 256, device="cuda")
+    ss = torch.empty(M, H // 1024, device="cuda")
     ops.norm_residual_mx(r, w, q, qs, ss, partials=part, nsplit=nsplit)
     assert torch.equal(r, want)
     q_ref, s_ref = _mx_quant(want * (1 + w))
     assert torch.equal(qs, s_ref)
     assert torch.equal(q, q_ref)
-    assert torch.allclose(ss, want.view(M, H // 256, 256).pow(2).sum(-1), rtol=1e-5, atol=0)
+    assert torch.allclose(ss, want.view(M, H // 1024, 1024).pow(2).sum(-1), rtol=1e-5, atol=0)
     r2 = resid.clone()
     ops.norm_residual_mx(r2, w, q, qs, ss, partials=part, nsplit=nsplit, write_resid=False)
     assert torch.equal(r2, resid)
@@ -1066,6 +1066,12 @@ def test_mx_norm_rows_and_rstd_consumers(M, H, nsplit, I):
     gu8, gus = quant_rows_fp8(Wgu)
     h8 = torch.empty(M, I, dtype=torch.uint8, device="cuda")
     hs = torch.empty(M * I // 32, dtype=torch.uint8, device="cuda")
+    if H // 128 not in (8, 16):     # MX rows in + MX h out need the wide form's compile-time 8 or 16 chunks
+        from pghip import _lib
+        with pytest.raises(_lib.PgHipError):
+            ops.gemm8(q, None, frag_pack8(gu8), gus, h8, epi=ops.EPI_BF16_GELU_MUL, M=M, frag=True, mx_in=qs,
+                      ss_in=ss, mx_out=hs)
+        return
     ops.gemm8(q, None, frag_pack8(gu8), gus, h8, epi=ops.EPI_BF16_GELU_MUL, M=M, frag=True, mx_in=qs, ss_in=ss,
               mx_out=hs)
     gg = (rstd * (xd @ _deq(gu8, gus).double().t())).float().view(M, I // 16, 2, 16)
