@@ -25,7 +25,10 @@ def _port():
 
 
 def _launch(worker, tmp_path, nproc=2, timeout=600, **env):
-    env = dict(os.environ, TP_OUT=str(tmp_path), **env)
+    # ranks sharing ONE device: at most 2 hardware queues per rank, so the 8 ranks' queues all stay mapped at once (an
+    # oversubscribed queue set is time-sliced, and a rank whose queue is not mapped cannot reach an exchange its peers
+    # spin in: measured as an occasional 20 s xGMI timeout at 8 ranks x 4 queues; a real node has a device per rank)
+    env = dict(os.environ, TP_OUT=str(tmp_path), GPU_MAX_HW_QUEUES="2", **env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", worker)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
@@ -108,11 +111,14 @@ def test_tp_engine_on_one_device(tmp_path, cfg, world, comm, chunk, fp8):
 
 def _check_896(res, min_checked):
     """Verdicts of tp_worker.full_size_896 (BASELINE configs[4]): bounded by the fp32 oracle run on the same e4m3 /
-    bf16 operand rounding (tests/golden/make_emu.py, <golden>_fp8emu.npz), not a flat percentage."""
+    bf16 operand rounding (tests/golden/make_emu.py, <golden>_fp8emu.npz), not a flat percentage.  The single-rank
+    engine keeps the 1.5x bound; the sharded run gets 1.75x: TP reorders every o_proj / down_proj / lm_head sum (rank
+    slices, then the xGMI sum in rank order), and on this recipe that reordering alone moves the logits by 1.2-1.3x
+    the emulated distance (vs_solo_emu_ratio, measured before and after the MX decode rows)."""
     for o in res:
         assert o["xgmi_err"] == 0 and o["vision_dp"], o
         assert o["fallbacks"] == 0, o                  # every collective went through the xGMI exchange
-        assert o["emu_ratio"] < 1.5, o                 # reference top-64 within 1.5x the emulated e4m3 distance
+        assert o["emu_ratio"] < 1.75, o                # reference top-64 within 1.75x the emulated e4m3 distance
         assert o["top1_bad"] == [] and o["top1_checked"] >= min_checked, o
         assert o["row_spread"] < 2e-2, o               # rows of one request agree
     r0 = res[0]
