@@ -3,6 +3,8 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-suite}; mkdir -p $O
+(while true; do sleep 60; echo "heartbeat $(date +%T)"; done) & HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1
 rc=$?; tail -4 $O/tests.log; [ $rc -eq 0 ] || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && tail -1 $O/smoke.log || exit 1
