@@ -1,0 +1,16 @@
+# round 5: 8-wave batched decode attention (tests + pt-896 x32 fp8 / pt-448 x16 decode A/B) (gpurun_out/$1)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=gpurun_out/${1:-nw8}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  tests/test_kernels_gpu.py -k "attn_decode_fused" > $O/tests.log 2>&1
+rc=$?; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/tests.log | tail -8; [ $rc -eq 0 ] || exit 1
+for r in 1 2; do
+  for nw in 8 4; do
+    PG_DECODE_NW=$nw timeout -k 10 300 python scripts/tune/decode_step.py --config pt-896 --batch 32 --fp8 --steps 50 \
+      2>> $O/err.log | sed "s/^{/{\"nw\": $nw, \"cfg\": \"pt896x32\", /" | tee -a $O/decode.jsonl || exit 1
+    PG_DECODE_NW=$nw timeout -k 10 300 python scripts/tune/decode_step.py --config pt-448 --batch 16 --steps 50 \
+      2>> $O/err.log | sed "s/^{/{\"nw\": $nw, \"cfg\": \"pt448x16\", /" | tee -a $O/decode.jsonl || exit 1
+  done
+done
