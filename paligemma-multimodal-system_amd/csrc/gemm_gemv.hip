@@ -489,13 +489,13 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int n0 = min((tile0 + t) * 16, e.N - 16) + 4 * g;
-      fin_r[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (!e.f.fx) fin_r[t] = *(const f32x4*)(e.f.fin_resid + (size_t)(r < M ? r : M - 1) * e.N + n0);
-      if (e.f.fx) {
-        const long long* p = e.f.fx + (size_t)(r < M ? r : M - 1) * e.N + n0;
-        fin_fa[t] = *(const i64x2*)p;
-        fin_fb[t] = *(const i64x2*)(p + 2);
-      }
+      const size_t ro = (size_t)(r < M ? r : M - 1) * e.N + n0;
+      // both loads unconditional (a branch or select on them here would make the compiler wait for them before
+      // the weight stream): without fx the fixed-point pair reads fin_resid's first 32 bytes, unused; fin_base picks
+      fin_r[t] = *(const f32x4*)(e.f.fin_resid + ro);
+      const long long* p = e.f.fx ? e.f.fx + ro : (const long long*)e.f.fin_resid;
+      fin_fa[t] = *(const i64x2*)p;
+      fin_fb[t] = *(const i64x2*)(p + 2);
       // (no select on a loaded value -- it would make the compiler wait right here: a null norm_w reads the
       // residual row instead, unused)
       fin_w[t] = *(const f32x4*)((e.f.norm_w ? e.f.norm_w : e.f.fin_resid) + n0);
@@ -616,10 +616,9 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
     // whole residual (its entries are cleared by this tile's finalising workgroup: every split of the tile loaded
     // them before its ticket)
     auto fin_base = [&](int t) {
-      f32x4 b = fin_r[t];
-      if (f.fx) b += f32x4{fx_to_f32(fin_fa[t][0]), fx_to_f32(fin_fa[t][1]), fx_to_f32(fin_fb[t][0]),
-                           fx_to_f32(fin_fb[t][1])};
-      return b;
+      return f.fx ? f32x4{fx_to_f32(fin_fa[t][0]), fx_to_f32(fin_fa[t][1]), fx_to_f32(fin_fb[t][0]),
+                          fx_to_f32(fin_fb[t][1])}
+                  : fin_r[t];
     };
     auto fx_clear = [&](int n0) {
       if (f.fx) {
