@@ -89,6 +89,9 @@ class PaliGemmaEngine:
                               # Unsplit won earlier this round (1.120-1.122 vs 1.123-1.127 ms/token); with the q|k|v
                               # weights Infinity-Cache resident split 2 wins 7 of 8 interleaved pairs, -3.7 us mean
                               # (scripts/r02/gpu_s3r.sh)
+    # 5..16 rows on the in-kernel-finalised path (F32_FIN): o_proj unsplit and down_proj split 4 (pt-448 x16: 1.391 vs
+    # 1.405 ms/step at 2 / 8, profiles/r05_decode_splits_pt448x16.jsonl); PG_SPLIT_O / PG_SPLIT_DOWN override
+    DECODE_SPLIT_O_FIN16, DECODE_SPLIT_DOWN_FIN16 = 1, 4
     DECODE_SPLIT_DOWN = 8   # split-K of down_proj at decode (8 vs 4: -4..6 us per pt-224 step, scripts/r02/gpu_t.sh)
     DECODE_SPLIT_KEYS = 32  # keys per wave in split-KV decode attention (one MFMA block)
     # keys per split at B <= FUSE_MAX_B: every o_proj workgroup merges all active splits in its prologue, so
@@ -751,6 +754,11 @@ class PaliGemmaEngine:
         H, nh, nkv, hd = w.hidden, w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
         so, sd = self._split_o(B), self.split_down
+        if B > self.FUSE_MAX_B and self.tp == 1:
+            if not os.environ.get("PG_SPLIT_O"):
+                so = self.DECODE_SPLIT_O_FIN16
+            if not os.environ.get("PG_SPLIT_DOWN"):
+                sd = self.DECODE_SPLIT_DOWN_FIN16
         tiles = (H + 15) // 16
         n_ss = tiles if B <= 4 else (tiles + 1) // 2         # one entry per GEMV workgroup (M > 4: tile pairs)
         merge_in_gemv = B <= self.FUSE_MAX_B
