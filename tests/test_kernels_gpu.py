@@ -896,7 +896,9 @@ def test_norm_residual_fp8_equals_quantised_bf16_output(M, H, nsplit):
                                       # ragged K splits (the runtime-trip-count forms, CPW = 0): K-split and wide
                                       # kernels; and more splits than 128-k chunks (the last splits own none)
                                       (20, 1024, 1152, 2), (32, 4096, 2048, 3), (20, 16384, 1152, 2),
-                                      (24, 512, 256, 4), (24, 16384, 256, 4)])
+                                      (24, 512, 256, 4), (24, 16384, 256, 4),
+                                      # an lm_head-sized grid (8192 tiles)
+                                      (20, 131072, 1024, 1)])
 def test_gemv8_fragment_packed_matches_the_fp8_tile_gemm(M, N, K, ks):
     """The fp8 weight-streaming GEMV (fragment-packed e4m3 weights, weights.frag_pack8; 17..32-row batched decode and
     the fp8 lm_head): equal to a torch fp32 matmul of the dequantised operands up to fp32 summation order, for the
