@@ -138,6 +138,10 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
 // PIPE: each wave's blocks are staggered -- the next block's K / V loads are issued between the current block's
 // phases, so its loads never drain during a compute phase (one wave per SIMD at pt-896 x32: each round's compute,
 // 0.9 us, stalled the stream of the single-buffered form).
+// splits whose partials the merging workgroup loads per round trip (8: the engine's split cap, no clamped duplicates)
+#ifndef PG_DEC_MERGE_MCH
+#define PG_DEC_MERGE_MCH 8
+#endif
 template <int DP, int DT, int NW, bool PIPE>
 __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs a, int nb, int* __restrict__ cnt,
                                                                       uint8_t* __restrict__ q8, float* __restrict__ q8s,
@@ -316,7 +320,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        // compiler-only: the loads stay below the ticket
   // the last split's workgroup merges the S partials: one thread per (q row, 8 dims), 16 splits per round trip
-  constexpr int D8 = DP / 8, MCH = 16;
+  constexpr int D8 = DP / 8, MCH = PG_DEC_MERGE_MCH;
   u32x4 pk = {0u, 0u, 0u, 0u};                      // this thread's last 8 outputs (the fp8 copy below)
   for (int it = threadIdx.x; it < G * D8; it += NW * 64) {
     const int r = it / D8, d8 = it % D8;
