@@ -138,6 +138,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
 // PIPE: each wave's blocks are staggered -- the next block's K / V loads are issued between the current block's
 // phases, so its loads never drain during a compute phase (one wave per SIMD at pt-896 x32: each round's compute,
 // 0.9 us, stalled the stream of the single-buffered form).
+#ifndef PG_DEC_SHARE_MERGE
+#define PG_DEC_SHARE_MERGE 1
+#endif
 // splits whose partials the merging workgroup loads per round trip (8: the engine's split cap, no clamped duplicates)
 #ifndef PG_DEC_MERGE_MCH
 #define PG_DEC_MERGE_MCH 8
@@ -263,22 +266,52 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
 #if PG_ATTN_STAMPS
   PG_STAMP(st1);
 #endif
-  // the NW waves' (O, m, l) -> the split's partial (wave 0), 2^(m_w - M) weights
-  __shared__ f32x4 so[NW > 1 ? NW - 1 : 1][DT][64];
-  __shared__ float sml[NW > 1 ? NW - 1 : 1][2][16];
+  // the NW waves' (O, m, l) -> the split's partial, 2^(m_w - M) weights.  SHARE (4 waves, DT % 4 == 0): every wave
+  // publishes its (O, m, l) and merges and stores a quarter of the columns (the same sum order as one wave merging
+  // all of them, so the same bits), so the partial's stores drain from four waves before the ticket
+  constexpr bool SHARE = PG_DEC_SHARE_MERGE && NW == 4 && DT % 4 == 0;
+  constexpr int NSO = SHARE ? NW : (NW > 1 ? NW - 1 : 1);
+  __shared__ f32x4 so[NSO][DT][64];
+  __shared__ float sml[NSO][2][16];
   __shared__ int s_last;
-  if (NW > 1 && wave > 0) {
+  if (SHARE || (NW > 1 && wave > 0)) {
+    const int ws = SHARE ? wave : wave - 1;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) so[wave - 1][t][lane] = o[t];
+    for (int t = 0; t < DT; ++t) so[ws][t][lane] = o[t];
     if (g == 0) {
-      sml[wave - 1][0][c] = m;
-      sml[wave - 1][1][c] = l;
+      sml[ws][0][c] = m;
+      sml[ws][1][c] = l;
     }
   }
   __syncthreads();
   const long pbase = ((long)b * a.Hkv + kvh) * S * 16;          // partial rows of (b, kv head): [S][16]
   const __amdgpu_buffer_rsrc_t ro = pg_rsrc(a.part_o + pbase * (DT * 16));
-  if (wave == 0) {
+  if constexpr (SHARE) {
+    float M = sml[0][0][c];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) M = fmaxf(M, sml[w][0][c]);
+    float ww[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) ww[w] = sml[w][0][c] == -INFINITY ? 0.f : exp2f(sml[w][0][c] - M);
+    float L = sml[0][1][c] * ww[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) L += ww[w] * sml[w][1][c];
+    if (c < G) {
+      const int row = sp * 16 + c;
+#pragma unroll
+      for (int t0 = 0; t0 < DT / NW; ++t0) {
+        const int t = wave * (DT / NW) + t0;
+        f32x4 v = so[0][t][lane] * ww[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) v += ww[w] * so[w][t][lane];
+        st16_sc1(ro, (row * (DT * 16) + 16 * t + 4 * g) * 4, v);
+      }
+      if (wave == 0 && g == 0)
+        __hip_atomic_store((pg_gu64*)(a.part_ml + (pbase + row) * 2), __builtin_bit_cast(unsigned long long,
+                           f32x2{M, L}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");             // every storing wave drained before the ticket
+  } else if (wave == 0) {
     float M = m;
 #pragma unroll
     for (int w = 0; w < NW - 1; ++w) M = fmaxf(M, sml[w][0][c]);
