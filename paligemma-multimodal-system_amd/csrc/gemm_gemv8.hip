@@ -17,18 +17,22 @@
 // MX: x rows carry E8M0 block scales (PgFusedArgs.mx_in, [M][4][K/128]).  The MFMA takes the scale of column r's
 // 32-k block b (k 32b .. 32b + 31 of the chunk, spread over lane groups 2(b % 2) and 2(b % 2) + 1) from lane (r, b), so
 // lane (r, g) loads block g's scale byte with its x bytes (no a_scale in the epilogue)
-template <int EPI, int NT, int MT, int DEPTH, int CPW, bool MX = false>
+// RS (row split, ksplit 1, MT 1): blockIdx.y picks the 16-row tile instead of a K split -- twice the workgroups for the
+// 17..32-row q|k|v GEMV, whose 160 tiles alone leave 96 CUs idle (each weight tile is read by two workgroups at once)
+template <int EPI, int NT, int MT, int DEPTH, int CPW, bool MX = false, bool RS = false>
 __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ X, int ldx,
                                                     const uint8_t* __restrict__ W, int K, EpiArgs e) {
+  static_assert(!RS || MT == 1, "row split: one 16-row tile per workgroup");
   amax_clear(e);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4, r = lane & 15;
+  const int g = lane >> 4, r0 = lane & 15;
+  const int r = (RS ? (int)blockIdx.y * 16 : 0) + r0;   // (the row of this lane's first row tile)
   const int tile0 = blockIdx.x * NT;
   const int M = e.M;
-  const int z = blockIdx.y;
+  const int z = RS ? 0 : blockIdx.y;
   const int nch_all = K >> 7;
-  const int per_z = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int per_z = RS ? nch_all : (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = z * per_z;
   const int nch = min(nch_all - c0, per_z);
   const int mine = CPW > 0 ? CPW : (nch > wave ? (nch - wave + 3) / 4 : 0);   // chunks wave, wave + 4, ...
@@ -453,24 +457,34 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
 #ifndef PG_GEMV8_DEPTH
 #define PG_GEMV8_DEPTH 4
 #endif
-template <int EPI, int NT, int MT, bool MX = false>
+template <int EPI, int NT, int MT, bool MX = false, bool RS = false>
 static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
-  const dim3 grid(((e.N >> 4) + NT - 1) / NT, ksplit);
+  const dim3 grid(((e.N >> 4) + NT - 1) / NT, RS ? (e.M + 15) / 16 : ksplit);
   const int nch = K >> 7;
   const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
   constexpr int D = PG_GEMV8_DEPTH;                // chunks in flight per wave
   switch (cpw) {
-    case 2: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, 2, 2, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    case 4: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 4, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    case 8: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 8, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
-    default: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 0, MX>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 2: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, 2, 2, MX, RS>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 4: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 4, MX, RS>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    case 8: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 8, MX, RS>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
+    default: hipLaunchKernelGGL((gemv8_kernel<EPI, NT, MT, D, 0, MX, RS>), grid, dim3(256), 0, st, X, ldx, W, K, e); break;
   }
 }
 
+#ifndef PG_GEMV8_ROWSPLIT
+#define PG_GEMV8_ROWSPLIT 1
+#endif
 template <int EPI, int NT>
 static void launch_gemv8_nt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
+  if constexpr (EPI == PG_EPI_QKV_ROPE) {
+    if (PG_GEMV8_ROWSPLIT && ksplit == 1 && e.M > 16) {
+      if (e.f.mx_in) launch_gemv8_mt<EPI, NT, 1, true, true>(X, ldx, W, K, 1, e, st);
+      else launch_gemv8_mt<EPI, NT, 1, false, true>(X, ldx, W, K, 1, e, st);
+      return;
+    }
+  }
   if (e.f.mx_in) {
     if (e.M <= 16) launch_gemv8_mt<EPI, NT, 1, true>(X, ldx, W, K, ksplit, e, st);
     else launch_gemv8_mt<EPI, NT, 2, true>(X, ldx, W, K, ksplit, e, st);
