@@ -17,8 +17,8 @@
 // MX: x rows carry E8M0 block scales (PgFusedArgs.mx_in, [M][4][K/128]).  The MFMA takes the scale of column r's
 // 32-k block b (k 32b .. 32b + 31 of the chunk, spread over lane groups 2(b % 2) and 2(b % 2) + 1) from lane (r, b), so
 // lane (r, g) loads block g's scale byte with its x bytes (no a_scale in the epilogue)
-// RS (row split, ksplit 1, MT 1): blockIdx.y picks the 16-row tile instead of a K split -- twice the workgroups for the
-// 17..32-row q|k|v GEMV, whose 160 tiles alone leave 96 CUs idle (each weight tile is read by two workgroups at once)
+// RS (row split, MT 1): blockIdx.z picks the 16-row tile -- twice the workgroups for the 17..32-row q|k|v GEMV, whose
+// 160 tiles alone leave 96 CUs idle, and for the o_proj's 256 (each weight tile is read by two workgroups at once)
 template <int EPI, int NT, int MT, int DEPTH, int CPW, bool MX = false, bool RS = false>
 __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ X, int ldx,
                                                     const uint8_t* __restrict__ W, int K, EpiArgs e) {
@@ -27,12 +27,12 @@ __global__ __launch_bounds__(256) void gemv8_kernel(const uint8_t* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, r0 = lane & 15;
-  const int r = (RS ? (int)blockIdx.y * 16 : 0) + r0;   // (the row of this lane's first row tile)
+  const int r = (RS ? (int)blockIdx.z * 16 : 0) + r0;   // (the row of this lane's first row tile)
   const int tile0 = blockIdx.x * NT;
   const int M = e.M;
-  const int z = RS ? 0 : blockIdx.y;
+  const int z = blockIdx.y;
   const int nch_all = K >> 7;
-  const int per_z = RS ? nch_all : (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
+  const int per_z = (nch_all + (int)gridDim.y - 1) / (int)gridDim.y;
   const int c0 = z * per_z;
   const int nch = min(nch_all - c0, per_z);
   const int mine = CPW > 0 ? CPW : (nch > wave ? (nch - wave + 3) / 4 : 0);   // chunks wave, wave + 4, ...
@@ -460,7 +460,7 @@ static void launch_gemv8x_mt(const uint8_t* X, int ldx, const uint8_t* W, int K,
 template <int EPI, int NT, int MT, bool MX = false, bool RS = false>
 static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
-  const dim3 grid(((e.N >> 4) + NT - 1) / NT, RS ? (e.M + 15) / 16 : ksplit);
+  const dim3 grid(((e.N >> 4) + NT - 1) / NT, ksplit, RS ? (e.M + 15) / 16 : 1);
   const int nch = K >> 7;
   const int cpw = (nch % ksplit == 0 && (nch / ksplit) % 4 == 0) ? nch / ksplit / 4 : 0;
   constexpr int D = PG_GEMV8_DEPTH;                // chunks in flight per wave
@@ -478,10 +478,11 @@ static void launch_gemv8_mt(const uint8_t* X, int ldx, const uint8_t* W, int K, 
 template <int EPI, int NT>
 static void launch_gemv8_nt(const uint8_t* X, int ldx, const uint8_t* W, int K, int ksplit, const EpiArgs& e,
                             hipStream_t st) {
-  if constexpr (EPI == PG_EPI_QKV_ROPE) {
-    if (PG_GEMV8_ROWSPLIT && ksplit == 1 && e.M > 16) {
-      if (e.f.mx_in) launch_gemv8_mt<EPI, NT, 1, true, true>(X, ldx, W, K, 1, e, st);
-      else launch_gemv8_mt<EPI, NT, 1, false, true>(X, ldx, W, K, 1, e, st);
+  if constexpr (EPI == PG_EPI_QKV_ROPE || EPI == PG_EPI_F32) {
+    // (a grid short of two workgroups per CU: the row split doubles it)
+    if (PG_GEMV8_ROWSPLIT && e.M > 16 && ((e.N >> 4) + NT - 1) / NT * ksplit < 512) {
+      if (e.f.mx_in) launch_gemv8_mt<EPI, NT, 1, true, true>(X, ldx, W, K, ksplit, e, st);
+      else launch_gemv8_mt<EPI, NT, 1, false, true>(X, ldx, W, K, ksplit, e, st);
       return;
     }
   }

@@ -9,7 +9,7 @@ timeout -k 10 900 python -u -m pytest -m gpu -v --timeout 600 --timeout-method t
   tests/test_kernels_gpu.py tests/test_engine_gpu.py tests/test_large_gpu.py -k "gemv8 or mx_ or fp8" > $O/tests.log 2>&1
 rc=$?; grep -E "passed|failed" $O/tests.log | tail -1; grep -E "emulated" $O/tests.log | head -3; [ $rc -eq 0 ] || exit 1
 for r in 1 2 3; do
-  for lib in "" scripts/tune/libs/rs0.so; do
+  for lib in "" scripts/tune/libs/rsq.so; do
     PGHIP_LIB=$lib timeout -k 10 300 python scripts/tune/decode_step.py --config pt-896 --batch 32 --fp8 --steps 50 \
       2>> $O/err.log | tee -a $O/decode.jsonl || exit 1
   done
