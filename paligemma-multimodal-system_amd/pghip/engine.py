@@ -150,7 +150,7 @@ class PaliGemmaEngine:
     HQ_CHUNKS = int(os.environ.get("PG_HQ_CHUNKS", "8"))
     # B > FUSE_MAX_B: split-KV attention and its merge in one launch (pg_attn_decode; 0 = split kernel + combine)
     DECODE_FUSED_ATTN = os.environ.get("PG_DECODE_FUSED", "1") != "0"
-    FUSED_MIN_ROUNDS = int(os.environ.get("PG_FUSED_MIN_ROUNDS", "3"))   # ... used from this many rounds per split on
+    FUSED_MIN_ROUNDS = int(os.environ.get("PG_FUSED_MIN_ROUNDS", "2"))   # ... used from this many rounds per split on
     # fp8 decode (> 16 rows): the one-launch attention also writes its rows as e4m3 for the fp8 o_proj (no
     # pg_quant_fp8 launch; same bytes)
     ATTN_FP8_OUT = os.environ.get("PG_ATTN_FP8_OUT", "1") != "0"
@@ -703,9 +703,10 @@ class PaliGemmaEngine:
         nh, nkv, hd = w.heads, w.kv_heads, w.head_dim
         kvd = nkv * hd
         # the one-launch kernel where the cache needs several rounds of waves (pt-896 x32: 34.3 vs 43.3 us per layer,
-        # attention + merge); with one or two rounds its last split's serial merge of every partial (64 KB read by
-        # one CU) costs more than the combine launch: pt-448 x16 1.429 vs 1.412 ms/step, pt-224 x16 1.374 vs
-        # 1.350 (scripts/gpu_ab_fused.sh, interleaved, one box)
+        # attention + merge); with one round its last split's serial merge of every partial costs more than the
+        # combine launch (pt-224 x16 1.374 vs 1.350 ms/step, round 4).  Since round 5's cheaper merge tail (8 partials
+        # per round trip, the four waves storing the split's partial) two rounds win too: pt-448 x16 1.348-1.351 vs
+        # 1.391-1.392 ms/step (profiles/r05_fused_attn_pt448_ab.jsonl; round 4 measured 1.429 vs 1.412)
         plan = ops.decode_plan(B, nkv, cache.Smax)
         if self.DECODE_FUSED_ATTN and hd in (32, 256) and cache.Smax >= 64 and plan[2] >= self.FUSED_MIN_ROUNDS:
             x8 = None
