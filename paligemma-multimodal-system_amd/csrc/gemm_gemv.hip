@@ -46,6 +46,9 @@
 #ifndef PG_GEMV_LM_D
 #define PG_GEMV_LM_D 6    // ... and that form's chunks in flight
 #endif
+#ifndef PG_GEMV_FIN_NT
+#define PG_GEMV_FIN_NT 2  // (tuning) 16-column tiles per workgroup of the finalised batched (M > 4) GEMV: 2 or 4
+#endif
 #ifndef PG_GEMV_D1
 #define PG_GEMV_D1 8      // chunks in flight of the one-tile GEMV (M <= 4: batch-1 decode o / down / q|k|v / lm_head)
 #endif
@@ -814,6 +817,12 @@ static void launch_gemv_pro(const bf16_t* A, int lda, const bf16_t* W, int ldw, 
   if constexpr (PG_GEMV_LM_NT == 2 && EPI == PG_EPI_F32) {
     if (e.M <= 4 && ntiles >= 8192 && ksplit == 1) {   // (tuning) the lm_head at batch 1-4 with two tiles per workgroup
       launch_gemv_cpw<EPI, 2, PG_GEMV_LM_D, PRO, FRAG>(dim3((ntiles + 1) / 2, 1), lds, st, A, lda, W, ldw, K, 1, e);
+      return;
+    }
+  }
+  if constexpr (PG_GEMV_FIN_NT == 4 && EPI == PG_EPI_F32_FIN) {
+    if (e.M > 4 && ntiles % 4 == 0) {   // (tuning) the finalised batched down GEMV with four tiles per workgroup
+      launch_gemv_cpw<EPI, 4, PG_GEMV_D2, PRO, FRAG>(dim3(ntiles / 4, ksplit), lds, st, A, lda, W, ldw, K, ksplit, e);
       return;
     }
   }
