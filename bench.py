@@ -345,6 +345,34 @@ def tp_specs(world):
 PROMPT = [2, 651, 4906, 603, 476, 2121, 576, 108]
 
 
+def _launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` (N > 1) run without a launcher: the same command as N ranks under
+    `python -m torch.distributed.run --nproc-per-node N` on 127.0.0.1, as a CHILD process (the parent has made no HIP
+    call and never execs).  Rank 0's JSON line is relayed to stdout; everything else the job prints goes to stderr.
+    Returns the job's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"[bench] --gpus {n}: launching {n} ranks: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    relayed = 0
+    for line in proc.stdout:
+        if line.startswith("{") and '"metric"' in line and not relayed:
+            print(line.rstrip("\n"), flush=True)
+            relayed += 1
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and not relayed:
+        log("[bench] the rank job printed no JSON line")
+        return 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -371,7 +399,16 @@ def main():
                     "instead of greedy, as BASELINE configs[3]")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the N ranks as a child torch.distributed.run job (nothing here has touched the
+        # GPU yet, and the parent never does), relay rank 0's JSON line and exit with the job's return code
+        sys.exit(_launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} from the launcher but --gpus {args.gpus}: they must agree "
+                         "(one rank per GPU)")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # PG_BENCH_BACKEND=gloo rehearses the multi-rank code paths with several ranks on one GPU

@@ -21,7 +21,8 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 11: PgFusedArgs mx_out / mx_in (MX block-scaled fp8 decode MLP rows); 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
+int pg_abi_version(void);   /* 12: PgFusedArgs.status (FX_ADD range check), amax_zero on the bf16 GEMV, the xGMI
+                              reduce-scatter + all-gather (pg_allreduce_xgmi_rs) and err diagnostics; 11: PgFusedArgs mx_out / mx_in (MX block-scaled fp8 decode MLP rows); 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
  * from (pghip/build.py).  The Python loader refuses a library whose hash differs from the tree it runs from.
@@ -101,7 +102,9 @@ typedef struct PgFusedArgs {
                                quantised to e4m3 while staged, row scale s[m] = amax_in[m * amax_ld] / 448 (1 when
                                zero) -- pg_quant_fp8's bytes and scale; a_scale is not read                          */
   int amax_ld;
-  unsigned* amax_zero;      /* optional, any PG_FP8|PG_W_FRAG launch: amax_zero[0 .. amax_zero_n) set to 0 (n <= 4096) */
+  unsigned* amax_zero;      /* optional, any PG_FP8|PG_W_FRAG launch: amax_zero[0 .. amax_zero_n) set to 0 (n <= 4096);
+                               (ABI 12) any bf16 PG_W_FRAG GEMV (M <= 16): the same after its weight stream, n <= 16384,
+                               n % 4 == 0, 16-B aligned (the batch-1 decode's first GEMV clears the fx accumulator)  */
   int amax_zero_n;
   /* ABI 10: */
   int64_t* fx;              /* fixed-point residual accumulator [M][K] (value = q * 2^-32, |value| < 2^31) written by
@@ -119,9 +122,13 @@ typedef struct PgFusedArgs {
                                clamped to [-127, 127] (e4m3 RNE of h / 2^e)                                          */
   const uint8_t* mx_in;     /* PG_FP8|PG_W_FRAG (any epilogue but F32_ADD), M <= 32, pro_mode 0: A is e4m3 [M][lda]
                                with mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale
-                               is not read.  With ss_in (rows from pg_norm_residual_mx, ss_n = K/256, eps) the outputs
-                               are multiplied by the row's rstd = rsqrt(sum ss_in[m*ss_ld + i] / K + eps), ss_n =
-                               K / 1024 <= 4                                                                        */
+                               is not read.  With ss_in (rows from pg_norm_residual_mx: sums of squares per 1024
+                               columns, ss_n = K / 1024 <= 4, eps) the outputs are multiplied by the row's
+                               rstd = rsqrt(sum ss_in[m*ss_ld + i] / K + eps)                                       */
+  /* ABI 12: */
+  int* status;              /* PG_EPI_FX_ADD (optional): set to 1 when an added value is non-finite or |v| >= 2^31; the
+                               value is then saturated (+-2^30 as the accumulator's value, NaN as 0), so a caller that
+                               finds *status set must treat the launch's results as invalid                           */
 } PgFusedArgs;
 
 /* Weight layout flag, OR-ed into `epi` of pg_gemm / pg_gemm_fused.  PG_W_FRAG: W is fragment-packed,
@@ -286,9 +293,12 @@ int pg_xgmi_ipc_close(void* p);
 /* In-place SUM of data[0, n) fp32 over `world` ranks (<= 8): every rank stores its data into slot `rank`
  * of every peer's buffer, raises a per-workgroup flag there, waits for the peers' flags in its own buffer
  * and sums the slots in rank order 0..world-1 (bit-identical result on every rank).  epochs: 64 local
- * zero-initialised u32 words owned by the communicator; err: a local int set to 1 if a peer did not
- * arrive within 20 s.  n % 4 == 0, n <= cap, data 16-byte aligned.  Device-side state only, so the call
- * can be captured into a hipGraph; every rank must issue the same sequence of calls. */
+ * zero-initialised u32 words owned by the communicator; err: 8 local ints (ABI 12), err[0] set to 1 if a peer did
+ * not arrive within 20 s, and the first timeout's diagnostics in err[1..6]: kind (1 one-shot, 2 reduce-scatter,
+ * 3 all-gather phase of pg_allreduce_xgmi_rs), workgroup, peer rank waited for, epoch expected, flag value seen, this
+ * rank.  Once err[0] is set later calls skip their waits (results invalid).  n % 4 == 0, n <= cap, data 16-byte
+ * aligned.  Device-side state only, so the call can be captured into a hipGraph; every rank must issue the same
+ * sequence of calls. */
 int pg_allreduce_xgmi(float* data, long n, int rank, int world, void* const* peers, long cap,
                       unsigned* epochs, int* err, hipStream_t stream);
 /* (ABI 8) The same SUM where each rank contributes the sum of its nslab (1..64) split-K slabs
@@ -301,6 +311,17 @@ int pg_allreduce_xgmi_slabs(float* data, long n, int nslab, long slab_stride, in
  * 16-byte aligned; otherwise as pg_allreduce_xgmi, whose buffer and epochs it shares (calls may interleave). */
 int pg_allgather_xgmi(const float* in, long n, float* out, int rank, int world, void* const* peers, long cap,
                       unsigned* epochs, int* err, hipStream_t stream);
+/* (ABI 12) Large messages (the prefill's row-chunk all-reduces after o_proj / down_proj, modeling_gemma.py:356 and
+ * :218 split across ranks; up to 32 MB): reduce-scatter + all-gather over a second buffer per rank of
+ * pg_xgmi_rs_buffer_bytes(world, rs_cap) bytes (allocated, exported and mapped like the exchange buffer).  Chunks of
+ * world x 1024 floats; rank p sums sub-piece p of every chunk in rank order (the same bits as pg_allreduce_xgmi_slabs)
+ * and stores it into every rank's gather slot.  2(W-1)/W * n floats leave each rank instead of (W-1) * n.
+ * nslab / slab_stride as pg_allreduce_xgmi_slabs; nwg (1..256) workgroups, the same on every rank and call (a workgroup
+ * waits only for the same workgroup of its peers: no grid-wide co-residency needed); epochs: 256 local zero-initialised
+ * u32 words owned by this RS buffer; err as above.  n % 4 == 0, n <= rs_cap, data 16-byte aligned. */
+int pg_xgmi_rs_buffer_bytes(int world, long rs_cap, long* bytes);
+int pg_allreduce_xgmi_rs(float* data, long n, int nslab, long slab_stride, int rank, int world, void* const* peers,
+                         long rs_cap, int nwg, unsigned* epochs, int* err, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -352,7 +352,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_decode_fused_kernel(AttnArgs 
 #endif
   if (!s_last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");        // compiler-only: the loads stay below the ticket
-  // the last split's workgroup merges the S partials: one thread per (q row, 8 dims), 16 splits per round trip
+  // the last split's workgroup merges the S partials: one thread per (q row, 8 dims), MCH (8) splits per round trip
   constexpr int D8 = DP / 8, MCH = PG_DEC_MERGE_MCH;
   u32x4 pk = {0u, 0u, 0u, 0u};                      // this thread's last 8 outputs (the fp8 copy below)
   for (int it = threadIdx.x; it < G * D8; it += NW * 64) {

@@ -29,7 +29,11 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                (K / 128 / ksplit == 8 || K / 128 / ksplit == 16));
   if (f.amax_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.amax_ld >= 1 &&
                              ((K >> 7) + ksplit - 1) / ksplit * 128 <= 4096 && PG_GEMV8_WIDE);
-  if (f.amax_zero) PG_REQUIRE(fp8 && frag && f.amax_zero_n >= 0 && f.amax_zero_n <= 4096);
+  // (ABI 12: also the bf16 fragment-packed GEMV, which clears the batch-1 decode's fixed-point accumulator with it)
+  if (f.amax_zero) PG_REQUIRE(frag && f.amax_zero_n >= 0 &&
+                              (fp8 ? f.amax_zero_n <= 4096
+                                   : (M <= 16 && f.amax_zero_n <= 16384 && f.amax_zero_n % 4 == 0 &&
+                                      ((uintptr_t)f.amax_zero & 15) == 0)));
   if (f.pro_mode == 0 || f.pro_mode == 4) PG_REQUIRE(A != nullptr && lda >= K);
   // (M > 4 runs two 16-row tiles per workgroup: the per-row entries are loaded 16 per lane)
   if (f.pro_mode == 4) PG_REQUIRE(ksplit == 1 && f.ss_in && f.ss_n > 0 && f.ss_ld >= f.ss_n &&

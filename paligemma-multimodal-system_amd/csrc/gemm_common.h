@@ -71,6 +71,16 @@ __device__ __forceinline__ long long fx_from_f32(float v) {
 // (consumers convert every entry of a row in every workgroup, so this is 3 VALU ops instead of __ll2float_rn's 12:
 // q = hi * 2^32 + lo with hi = q >> 32 (arithmetic), lo the unsigned low word; value = hi + lo * 2^-32, rounded twice --
 // a fixed function of q's bits, so every reader gets the same float)
+// The range-checked form the FX_ADD epilogue uses: a value the accumulator cannot hold (|v| >= 2^31, or NaN / Inf) is
+// saturated to +-2^62 (NaN: 0) -- far outside any residual, without the int conversion's undefined behaviour -- and
+// reported through *status (PgFusedArgs.status, may be null)
+__device__ __forceinline__ long long fx_from_f32_checked(float v, int* status) {
+  if (__builtin_expect(!(fabsf(v) < 0x1p31f), 0)) {
+    if (status) atomicOr(status, 1);
+    return v > 0.f ? (1LL << 62) : (v < 0.f ? -(1LL << 62) : 0LL);
+  }
+  return fx_from_f32(v);
+}
 __device__ __forceinline__ float fx_to_f32(long long q) {
   return fmaf((float)(unsigned)(unsigned long long)q, PG_FX_INV, (float)(int)(q >> 32));
 }
@@ -148,6 +158,9 @@ struct PgFusedArgs {
   // is not read)
   uint8_t* mx_out;
   const uint8_t* mx_in;
+  // ABI 12: PG_EPI_FX_ADD status word (optional): set to 1 when an added value is non-finite or |v| >= 2^31 -- it is
+  // then saturated (the accumulator cannot hold it), so the caller must treat the step's results as invalid
+  int* status;
 };
 
 // 4 consecutive fp32 values at p[n0..n0+3] (one 16-B load when fully inside [0, N), else guarded)

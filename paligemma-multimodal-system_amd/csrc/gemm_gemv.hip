@@ -559,6 +559,11 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
 #pragma unroll
   for (int t = 0; t < NT; ++t) red[wave][t][lane] = acc[t];
   __syncthreads();
+  // PgFusedArgs.amax_zero (ABI 12 for this kernel): workgroup (0, 0) clears amax_zero[0 .. n) after its stream -- the
+  // batch-1 decode step's first GEMV zeroes the fixed-point accumulator that the step's FX_ADD producers add into,
+  // so no state carries over from an interrupted step (n % 4 == 0, 16-B aligned, host-checked)
+  if (e.f.amax_zero && gi.bx == 0 && gi.by == 0)
+    for (int i = 4 * (int)threadIdx.x; i < e.f.amax_zero_n; i += 1024) *(u32x4*)(e.f.amax_zero + i) = u32x4{0u, 0u, 0u, 0u};
   if (wave != 0) return;
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = red[0][t][lane] + red[1][t][lane] + red[2][t][lane] + red[3][t][lane];
@@ -740,7 +745,7 @@ __device__ __forceinline__ void gemv_body(const bf16_t* __restrict__ A, int lda,
           if (e.f.resid_in && z == 0) v += load4_guard(e.f.resid_in + (size_t)m * e.N, n0, e.N);
           unsigned long long* dst = (unsigned long long*)e.C + (size_t)m * e.ldc + n0;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) atomicAdd(dst + j, (unsigned long long)fx_from_f32(v[j]));
+          for (int j = 0; j < 4; ++j) atomicAdd(dst + j, (unsigned long long)fx_from_f32_checked(v[j], e.f.status));
         }
       }
     }

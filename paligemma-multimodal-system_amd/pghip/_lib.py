@@ -29,7 +29,7 @@ class PgFusedArgs(C.Structure):
                 ("slab_rows", C.c_int), ("kd", C.c_void_p), ("vd", C.c_void_p),
                 ("amax_out", C.c_void_p), ("amax_in", C.c_void_p), ("amax_ld", C.c_int), ("amax_zero", C.c_void_p),
                 ("amax_zero_n", C.c_int), ("fx", C.c_void_p),
-                ("mx_out", C.c_void_p), ("mx_in", C.c_void_p)]
+                ("mx_out", C.c_void_p), ("mx_in", C.c_void_p), ("status", C.c_void_p)]
 
 
 # name -> argtypes (every function returns int: 0 or a hipError_t code)
@@ -69,6 +69,8 @@ SIGNATURES = {
     "pg_allreduce_xgmi": [vp, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
     "pg_allreduce_xgmi_slabs": [vp, i64, i32, i64, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
     "pg_allgather_xgmi": [vp, i64, vp, i32, i32, C.POINTER(C.c_void_p), i64, vp, vp, vp],
+    "pg_xgmi_rs_buffer_bytes": [i32, i64, C.POINTER(C.c_long)],
+    "pg_allreduce_xgmi_rs": [vp, i64, i32, i64, i32, i32, C.POINTER(C.c_void_p), i64, i32, vp, vp, vp],
 }
 
 _lib = None
@@ -79,7 +81,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 def source_hash(lib=None) -> str:

@@ -732,6 +732,19 @@ class PaliGemmaEngine:
             return self.DECODE_SPLIT_O_SMALL
         return self.split_o
 
+    def fx_status(self) -> torch.Tensor:
+        """The fixed-point residual's status word (PgFusedArgs.status): an FX_ADD launch sets it when a value is
+        non-finite or beyond the accumulator's +-2^31 range (saturated, so the step's results are invalid)."""
+        return self._zeros("d_fx_status", (1,), torch.int32)
+
+    def check_numerics(self):
+        """Raise if a decode step's fixed-point residual overflowed or received a NaN / Inf (one host read)."""
+        t = self._ws.get("d_fx_status")
+        if t is not None and int(t.item()):
+            t.zero_()
+            raise FloatingPointError("decode residual: a non-finite or out-of-range (|v| >= 2^31) value reached the "
+                                     "fixed-point accumulator; the generated tokens are invalid")
+
     def _zeros(self, name, shape, dtype):
         """Persistent zero-initialised buffer (e.g. self-resetting arrival tickets)."""
         t = self._ws.get(name)
@@ -775,6 +788,7 @@ class PaliGemmaEngine:
         # "fx": the partials go to the fixed-point accumulator (zero between steps: the last layer's F32_FIN clears it);
         # layer 0's o_proj also folds the embedding rows in, so from there on it holds the whole residual
         fx = self._zeros("d_fx", (B, H), torch.int64) if merge_in_gemv and self.DECODE_ADD == "fx" else None
+        fx_st = self.fx_status() if fx is not None else None      # set by an FX_ADD launch given an unholdable value
         add_epi, add_dst = (ops.EPI_FX_ADD, fx) if fx is not None else (ops.EPI_F32_ADD, res)
         for i, Lw in enumerate(w.tl):
             rope = dict(head_dim=hd, cos_t=cos_t, sin_t=sin_t, pos=st["pos"], rows_per_batch=1,
@@ -785,6 +799,10 @@ class PaliGemmaEngine:
                 # residual -- that launch folds res in -- and the consumers read it alone)
                 fa = ops.fused_args(pro_mode=ops.PRO_RMSNORM, resid_in=res if (i == 0 or fx is None) else None,
                                     fx=fx if i > 0 else None, nsplit=0, norm_w=Lw["in_w"], eps=1e-6, **rope)
+                if i == 0 and fx is not None:
+                    # the step starts from a zero accumulator whatever an earlier (interrupted) step left in it: layer 0's
+                    # q|k|v GEMV does not read it and clears it before layer 0's o_proj adds into it
+                    fa.amax_zero, fa.amax_zero_n = fx.data_ptr(), fx.numel() * 2
                 ops.gemm_fused(None, Lw["qkv_w"], qb, fa, epi=ops.EPI_QKV_ROPE | w.wflag, M=B)
             else:
                 fa = ops.fused_args(pro_mode=ops.PRO_X_RSTD, ss_in=ss_d, ss_ld=tiles, ss_n=n_ss, eps=1e-6, **rope)
@@ -798,7 +816,8 @@ class PaliGemmaEngine:
                 if add_o:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
                                         head_dim=hd, dtw=dt, q_per_kv=nh // nkv, kv_heads=nkv, slot_dev=st["kv_len"],
-                                        akeys=SK, resid_in=res if (fx is not None and i == 0) else None)
+                                        akeys=SK, resid_in=res if (fx is not None and i == 0) else None,
+                                        status=fx_st)
                     ops.gemm_fused(None, Lw["o_w"], add_dst, fa, epi=add_epi | w.wflag, M=B, ksplit=so)
                 else:
                     fa = ops.fused_args(pro_mode=ops.PRO_ATTN_COMBINE, part_o=part_o, part_ml=part_ml, asplit=nsplit,
@@ -813,11 +832,11 @@ class PaliGemmaEngine:
                 ops.gemm_fused(attn, Lw["o_w"], part, fa, epi=ops.EPI_F32_FIN | w.wflag, M=B, ksplit=so)
             nxt_w = w.tl[i + 1]["in_w"] if i + 1 < nl else w.final_w
             self._mlp_fin(Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd,
-                          add=add_down and i + 1 < nl, gu_rms=add_o, fx=fx)
+                          add=add_down and i + 1 < nl, gu_rms=add_o, fx=fx, fx_st=fx_st)
         return xq, ss_d, tiles, n_ss
 
     def _mlp_fin(self, Lw, xq, ss_o, tiles, n_ss, h, part, cnt, res, ss_d, nxt_w, B, sd, add=False, gu_rms=False,
-                 fx=None):
+                 fx=None, fx_st=None):
         """gate/up + down of a _decode_layers_fin layer: x' = xq with rstd from ss_o -> h -> down, finalised into res
         (x' of the next norm -> xq, its sums of squares -> ss_d).  add: down adds its partials into res with float
         atomics (EPI_F32_ADD), or into the fixed-point accumulator fx (EPI_FX_ADD); the next GEMV normalises res (+ fx)
@@ -832,7 +851,8 @@ class PaliGemmaEngine:
             ops.gemm_fused(xq, Lw["gu_w"], h, fa, epi=ops.EPI_BF16_GELU_MUL | w.wflag, M=B)
         if add:
             if fx is not None:
-                ops.gemm_fused(h, Lw["down_w"], fx, ops.fused_args(), epi=ops.EPI_FX_ADD | w.wflag, M=B, ksplit=sd)
+                ops.gemm_fused(h, Lw["down_w"], fx, ops.fused_args(status=fx_st), epi=ops.EPI_FX_ADD | w.wflag, M=B,
+                               ksplit=sd)
             else:
                 ops.gemm_fused(h, Lw["down_w"], res, ops.fused_args(), epi=ops.EPI_F32_ADD | w.wflag, M=B, ksplit=sd)
             return
@@ -1024,6 +1044,7 @@ class PaliGemmaEngine:
             step_fn()
             n += 1
         hist = st["hist"][:n].t().contiguous().cpu()
+        self.check_numerics()
         if hasattr(self.comm, "check"):
             self.comm.check()              # an xGMI exchange that timed out leaves meaningless sums: raise
         if stop_token is None:

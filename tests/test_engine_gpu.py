@@ -249,6 +249,46 @@ def test_pt224_decode_bit_reproducible_run_to_run(golden):
         assert not diff, f"logits differ at steps {diff}"
 
 
+def test_decode_step_starts_from_a_clean_fx_accumulator(tiny, golden):
+    """The batch-1 decode residual's fixed-point accumulator carries no state between steps: a step that
+    begins with garbage left in it -- as after an interrupted step -- gives the same logits, bit for bit, as a step from
+    a zero accumulator, because layer 0's q|k|v GEMV clears it (PgFusedArgs.amax_zero on the bf16 GEMV, ABI 12) before
+    any FX_ADD producer adds into it.  And a status word set by an overflowing FX_ADD makes generate() raise."""
+    eng, _ = tiny
+    assert eng.DECODE_ADD == "fx"
+    g = golden("tiny")
+    ids = torch.from_numpy(g["b1_input_ids"]).cuda()
+    px = torch.from_numpy(g["b1_pixel_values"]).cuda()
+    cache, feats, logits, nxt = eng.prefill_request(ids, px, torch.ones_like(ids), 8)
+    sampler = dict(do_sample=False)
+    st = eng.decode_state(1, cache, nxt, 8, sampler=sampler)
+    eng.sample(logits, st, sampler, advance=False, feats=feats)
+    eng.decode_step(st, cache, feats, sampler)                 # one step so every workspace exists
+    torch.cuda.synchronize()
+    snap = {k: st[k].clone() for k in ("ids", "pos", "kv_len", "step", "hist")}
+    res0 = eng._ws["d_res_a"].clone() if st.get("chain") else None
+
+    def step(dirty):
+        for k, v in snap.items():
+            st[k].copy_(v)
+        if res0 is not None:
+            eng._ws["d_res_a"].copy_(res0)
+        fx = eng._ws["d_fx"]
+        if dirty:
+            fx.copy_(torch.randint(-2 ** 40, 2 ** 40, fx.shape, dtype=torch.int64))
+        out = eng.decode_step(st, cache, feats, sampler).clone()
+        torch.cuda.synchronize()
+        assert int(fx.abs().sum()) == 0                        # the step's last layer leaves it zero again
+        return out
+
+    clean = step(False)
+    assert torch.equal(step(True), clean)
+    eng.fx_status().fill_(1)                                   # as an FX_ADD launch given an Inf would
+    with pytest.raises(FloatingPointError):
+        eng.generate(ids, px, torch.ones_like(ids), 4)
+    assert int(eng.fx_status().item()) == 0
+
+
 def test_batched_generation_per_row_eos(tiny, golden):
     """B = 2 rows of the same request (+ one different image): each row equals its own B = 1 run, cut at
     its own EOS (tokens after a row's EOS come back as pad)."""

@@ -55,7 +55,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.pg_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_library_matches_source_tree():
@@ -299,3 +299,17 @@ def test_engine_refuses_split_knobs_the_kernels_reject(monkeypatch):
     monkeypatch.setenv("PG_SPLIT_DOWN", "16")
     with pytest.raises(ValueError, match="split-K 16"):
         engine.PaliGemmaEngine(cfg, P, device="cpu")
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    """bench.py under a launcher whose WORLD_SIZE differs from --gpus fails loudly before touching the device (the
+    driver's N-GPU line must come from N ranks)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and "--gpus 4" in r.stderr, r.stderr[-2000:]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "--gpus must be >= 1" in r.stderr, r.stderr[-2000:]

@@ -1151,6 +1151,37 @@ def test_gemv_fx_add_fixed_point_residual(M, z, pro):
     assert all(torch.equal(runs[0], r) for r in runs[1:])
 
 
+def test_fx_add_range_check_sets_status():
+    """PG_EPI_FX_ADD's range check (ABI 12, PgFusedArgs.status): a partial the int64 accumulator cannot hold -- an Inf
+    or NaN from upstream, or |v| >= 2^31 -- is saturated (value +-2^30, NaN as 0) instead of wrapping through the
+    undefined float->int conversion, and the status word is set; in-range launches leave it zero and their rows
+    exact.  Row 0 is normal, row 1 gets an Inf in x (its dot products are +-Inf or NaN), row 2 a huge finite value."""
+    from pghip import ops
+    from pghip.weights import frag_pack
+    M, N, K = 3, 256, 2048
+    x = rnd(M, K, seed=40)
+    W = rnd(N, K, scale=1 / 45, seed=41)
+    Wk = frag_pack(W)
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(M, N, dtype=torch.int64, device="cuda")
+    ops.gemm_fused(x[:1], Wk, acc, ops.fused_args(status=st), epi=ops.EPI_FX_ADD | ops.W_FRAG, M=1, ksplit=2)
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
+    assert err((acc[0].double() / ops.FX_SCALE).float(), x[0].float() @ W.float().t()) < 1e-5
+    xb = x.clone()
+    xb[1, 5] = float("inf")
+    xb[2, :] = 3e4                                     # x.W ~ 3e4 * 2048 * |w| ~ 1e8 .. beyond 2^31 for some n
+    xb[2, :64] = 3e38
+    acc.zero_()
+    ops.gemm_fused(xb, Wk, acc, ops.fused_args(status=st), epi=ops.EPI_FX_ADD | ops.W_FRAG, M=M, ksplit=2)
+    torch.cuda.synchronize()
+    assert int(st.item()) == 1
+    v = acc.double() / ops.FX_SCALE
+    assert err(v[0].float(), x[0].float() @ W.float().t()) < 1e-5      # the in-range row is untouched
+    lim = 2.0 ** 31                                    # 2 splits x +-2^30 at most: a finite, flagged value
+    assert bool((v[1:].abs() <= lim).all()) and bool((v[1:].abs() >= 2 ** 29).any())
+
+
 @pytest.mark.parametrize("M", [1, 2])
 def test_fx_accumulator_consumers_rmsnorm_and_fin_clear(M):
     """The fixed-point accumulator's life in a decode step: an FX_ADD launch with resid_in folds the fp32 residual rows

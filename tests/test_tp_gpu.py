@@ -38,16 +38,20 @@ def _launch(worker, tmp_path, nproc=2, timeout=600, **env):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_ranks_on_one_device(tmp_path, world):
-    """pg_allreduce_xgmi / pg_allgather_xgmi between `world` processes sharing the device through IPC-mapped
-    exchange buffers (the 8-rank case is the TP=8 exchange of BASELINE configs[4]): bit-exact against the
-    rank-order fp32 sum / concatenation for ragged sizes (one and many workgroups, both buffer sets), back to
-    back with different sizes and no host sync, all-gathers interleaved with all-reduces, identical on every
-    rank, inside a captured hipGraph, and without a timeout."""
+    """pg_allreduce_xgmi / pg_allgather_xgmi / pg_allreduce_xgmi_rs between `world` processes sharing the device
+    through IPC-mapped exchange buffers (the 8-rank case is the TP=8 exchange of BASELINE configs[4]): bit-exact
+    against the rank-order fp32 sum / concatenation for ragged sizes (one and many workgroups, both buffer sets, the
+    one-shot and the reduce-scatter + all-gather form), back to back with different sizes and forms and no host sync,
+    split-K slabs summed on the way in, all-gathers interleaved with all-reduces, identical on every rank, inside a
+    captured hipGraph, and without a timeout.  Prints both forms' time for a 4 MB message on this shared device."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
     res = _launch("xgmi_worker.py", tmp_path, nproc=world)
+    print(json.dumps({"world": world, "timing": res[0]["timing"], "rs_wg": res[0]["rs_wg"]}))
     for o in res:
         assert o["err"] == 0, o
+        assert o["ranks_per_device"] == world and o["rs_wg"] == max(8, 256 // world), o
+        assert o["rs_calls"] > 0, o
         assert o["bad"] == [], o
         assert o["graph_bad"] == [], o
         assert o["seq_bad"] == [], o
@@ -157,6 +161,32 @@ def test_tp8_pt896_fp8_batch8(tmp_path):
                   TP_GOLDEN="pt896")
     print(json.dumps({k: v for k, v in res[0].items() if k != "top1"}))
     _check_896(res, min_checked=0)
+
+
+@pytest.mark.slow
+def test_bench_gpus2_launches_two_ranks():
+    """`python bench.py --gpus 2` with no launcher around it (the driver's N > 1 command line) starts two ranks as a
+    torch.distributed.run child and relays rank 0's line: n_gpus 2, the data-parallel value, and the tensor-parallel
+    legs (the headline request at TP=2, configs[3] top-p at TP=2, configs[4] pt-896 x32 fp8 at TP=2), none failed.
+    The two ranks share this one device over gloo (PG_BENCH_BACKEND=gloo); on the 8-GPU node the backend is RCCL."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs the HIP device")
+    env = dict(os.environ, PG_BENCH_BACKEND="gloo", GPU_MAX_HW_QUEUES="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=1100)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    print(json.dumps(rec))
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 2, rec
+    assert rec["value"] > 0 and rec["scaling"] == "weak", rec
+    for leg, tp in (("tp", 2), ("configs[3]", 2), ("configs[4]", 2)):
+        assert leg in rec and "error" not in rec[leg], rec.get(leg)
+        assert rec[leg]["tp"] == tp and rec[leg]["tokens_per_s"] > 0, rec[leg]
+    assert rec["configs[4]"]["fp8"] and rec["configs[4]"]["batch"] == 32
+    assert rec["configs[3]"]["sampler"].startswith("top-p")
 
 
 @pytest.mark.slow

@@ -186,6 +186,7 @@ def tiny(rank, world, name):
         out["fp8_decode24_intrinsic"] = max(ie)
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+    out["xgmi_diag"] = comm.diagnostics() if isinstance(comm, XgmiComm) else {}
     if isinstance(comm, XgmiComm):
         comm.close()
     with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
@@ -264,6 +265,7 @@ def full_size(rank, world, name):
                                            float(u[0, 0]))
     torch.cuda.synchronize()
     out["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+    out["xgmi_diag"] = comm.diagnostics() if isinstance(comm, XgmiComm) else {}
     if isinstance(comm, XgmiComm):
         comm.close()
     with open(os.path.join(os.environ["TP_OUT"], f"rank{rank}.json"), "w") as f:
@@ -341,6 +343,7 @@ def full_size_896(rank, world):
            "fallbacks": getattr(comm, "fallbacks", -1), "cap": getattr(comm, "cap", 0)}
     torch.cuda.synchronize()
     res["xgmi_err"] = int(comm.err.item()) if isinstance(comm, XgmiComm) else 0
+    res["xgmi_diag"] = comm.diagnostics() if isinstance(comm, XgmiComm) else {}
 
     def checks(lg):
         """Per (image, step, kept row): top-64 distance / the emulation's, and the top-1 checks where the reference's

@@ -1,6 +1,7 @@
-"""Rank body of tests/test_tp_gpu.py::test_xgmi_allreduce_two_ranks_on_one_device (torch.distributed.run,
-2 ranks on one HIP device; gloo only carries the IPC handles).  Every rank can regenerate every rank's
-seeded input, so each checks pg_allreduce_xgmi bit-exactly against the fp32 sum in rank order."""
+"""Rank body of tests/test_tp_gpu.py::test_xgmi_allreduce_ranks_on_one_device (torch.distributed.run, 2 / 4 / 8
+ranks on one HIP device; gloo only carries the IPC handles).  Every rank can regenerate every rank's seeded input, so
+each checks pg_allreduce_xgmi (one-shot, up to 2^15 elements here) and pg_allreduce_xgmi_rs (reduce-scatter +
+all-gather, above) bit-exactly against the fp32 sum in rank order, and times both forms on a 4 MB message."""
 import hashlib
 import json
 import os
@@ -29,10 +30,12 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     from pghip.tp import XgmiComm
-    comm = XgmiComm(cap=1 << 20)
+    # one-shot up to 2^15 elements, reduce-scatter + all-gather above (the product default switches at 2^18)
+    comm = XgmiComm(cap=1 << 20, rs_cap=1 << 21, rs_min=1 << 15)
     bad, dig = [], hashlib.sha256()
-    # ragged sizes: one workgroup, partial last chunk, many workgroups, the cap itself; each twice (both sets)
-    sizes = [4, 1000, 8192, 8196, 2048 * 16, 257216, 3 * 8192 * 64 + 4, 1 << 20] if world <= 2 else [4, 8196, 2048 * 16]
+    # ragged sizes: one workgroup, partial last chunk, many workgroups, the caps themselves; each twice (both sets)
+    sizes = ([4, 1000, 8192, 8196, 2048 * 16, 32772, 257216, 3 * 8192 * 64 + 4, 1 << 20, 1 << 21] if world <= 2 else
+             [4, 8196, 2048 * 16, 32772, 65540 + 8 * 1024 * 3, 1 << 20])
     for it, n in enumerate(sizes * 2):
         t = rank_data(n, rank, it).cuda()
         comm.all_reduce(t)
@@ -42,7 +45,7 @@ def main():
         dig.update(got.numpy().tobytes())
     # back to back without a host sync: one-chunk, multi-chunk-per-workgroup and cap-sized exchanges
     # interleaved, so a workgroup that reused a buffer set early would corrupt a peer's unread slots
-    seq = [2048, 600000, 4, 1 << 20, 2048, 524292, 8196, 1 << 20]
+    seq = [2048, 600000, 4, 1 << 20, 2048, 524292, 8196, 1 << 20, 1 << 21, 40000, 4, 1 << 21]
     ins = [rank_data(n, rank, 200 + i).cuda() for i, n in enumerate(seq)]
     torch.cuda.synchronize()
     dist.barrier()
@@ -50,6 +53,19 @@ def main():
         comm.all_reduce(t)
     torch.cuda.synchronize()
     seq_bad = [[n, i] for i, (n, t) in enumerate(zip(seq, ins)) if not torch.equal(t.cpu(), expected(n, world, 200 + i))]
+    # split-K slabs summed on the way in (slab order, then rank order), both forms
+    for it, n in enumerate([8192, 300004]):
+        ns = 3
+        part = torch.stack([rank_data(n, rank, 500 + 10 * it + s_) for s_ in range(ns)]).cuda()
+        comm.all_reduce_slabs(part, ns)
+        want = None
+        for r in range(world):
+            c = rank_data(n, r, 500 + 10 * it)
+            for s_ in range(1, ns):
+                c = c + rank_data(n, r, 500 + 10 * it + s_)
+            want = c if want is None else want + c
+        if not torch.equal(part[0].cpu(), want):
+            seq_bad.append(["slabs", n])
     # all-gather in rank order (pg_allgather_xgmi), interleaved with all-reduces on the same buffer / epochs
     gather_bad = []
     for it, n in enumerate([4, 2048, 32160, 8196, 1 << 20 if world <= 2 else 1 << 18]):
@@ -62,7 +78,7 @@ def main():
         if not torch.equal(out.cpu(), want) or not torch.equal(r.cpu(), expected(8, world, 400 + it)):
             gather_bad.append(n)
     # captured: three exchanges of different sizes in one graph, replayed with fresh inputs
-    sizes = [2048, 2048 * 16, 4 * 8192]
+    sizes = [2048, 2048 * 16, 4 * 8192, 131076]
     static = [torch.zeros(n, device="cuda") for n in sizes]
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -84,8 +100,27 @@ def main():
         for t, n in zip(static, sizes):
             if not torch.equal(t.cpu(), expected(n, world, it)):
                 graph_bad.append([n, rep])
-    out = {"rank": rank, "err": int(comm.err.item()), "bad": bad, "graph_bad": graph_bad, "seq_bad": seq_bad,
-           "gather_bad": gather_bad,
+    # timing of a 4 MB message (a 512-row prefill chunk) in both forms, ranks sharing this one device (no xGMI link is
+    # crossed here: the numbers bound the kernels' own cost, not the link rate)
+    timing = {}
+    t = torch.ones(1 << 20, device="cuda")
+    for form, rs_min in (("rs", comm.rs_min), ("oneshot", 1 << 30)):
+        saved, comm.rs_min = comm.rs_min, rs_min
+        ts = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            dist.barrier()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record()
+            comm.all_reduce(t)
+            ev[1].record()
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+        comm.rs_min = saved
+        timing[f"{form}_4MB_us"] = sorted(ts[1:])[len(ts[1:]) // 2]
+    out = {"rank": rank, "err": int(comm.err.item()), "diag": comm.diagnostics(), "bad": bad, "graph_bad": graph_bad,
+           "seq_bad": seq_bad, "gather_bad": gather_bad, "rs_calls": comm.rs_calls, "rs_wg": comm.rs_wg,
+           "ranks_per_device": comm.ranks_per_device, "timing": timing,
            "digest": dig.hexdigest()}
     del g
     comm.close()
