@@ -60,24 +60,33 @@ class bf16_operands:
 # rows (q|k|v, gate/up, the lm_head) take MX rows of the normalised input too (engine.MX_NORM: pg_norm_residual_mx
 # quantises x*(1+w) per 32-column block and the GEMV applies rstd to its outputs -- the same block-relative e4m3
 # rounding; emulated on the normalised row, so per-element bits differ where rstd is not a power of two).
+# tp=W (> 1): the tensor-parallel form of the HIP path (engine.tp): the row-parallel o_proj and
+# down_proj run on W equal K slices -- each rank quantises its slice of the activation row and its slice of every
+# weight row with their own max/448 scales (weights.PackedWeights(tp_world=W) / pg_quant_fp8 on the local slice; MX
+# blocks of 32 do not cross a slice) -- and the W partial products are summed in rank order (the xGMI exchange's
+# order).  The column-parallel q|k|v, gate/up and the vocabulary-parallel lm_head quantise whole rows exactly as at
+# W = 1, so they need nothing.
 _FP8_MIN_ROWS = None
 _FP8_LM_HEAD = False
 _FP8_MX_H = False
 _FP8_MX_NORM = False
+_FP8_TP = 1
 
 
 class fp8_operands:
-    def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False, mx_norm: bool = False):
-        self.min_rows, self.lm_head, self.mx_h, self.mx_norm = min_rows, lm_head, mx_h, mx_norm
+    def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False, mx_norm: bool = False,
+                 tp: int = 1):
+        self.min_rows, self.lm_head, self.mx_h, self.mx_norm, self.tp = min_rows, lm_head, mx_h, mx_norm, tp
 
     def __enter__(self):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM
-        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM)
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM = self.min_rows, self.lm_head, self.mx_h, self.mx_norm
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP
+        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP)
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP = (self.min_rows, self.lm_head, self.mx_h,
+                                                                          self.mx_norm, self.tp)
 
     def __exit__(self, *a):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM = self._old
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP = self._old
 
 
 def mx_exp(amax: np.ndarray) -> np.ndarray:
@@ -141,21 +150,34 @@ def layer_norm(x: np.ndarray, w: np.ndarray, b: np.ndarray, eps: float) -> np.nd
 
 
 def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: bool = False,
-           mx: str = "") -> np.ndarray:
+           mx: str = "", rowpar: bool = False) -> np.ndarray:
     """nn.Linear: x @ w.T + b.  (gemma: a Gemma decoder linear, for the fp8-operand emulation; mx: "h" for the
     down_proj, "x" for the RMSNorm-fed linears, whose <= 32-row calls take MX rows under fp8_operands(mx_h=True) /
-    (mx_norm=True).)"""
+    (mx_norm=True); rowpar: a row-parallel linear (o_proj, down_proj), sliced along K under fp8_operands(tp=W).)"""
     rows = x.size // x.shape[-1]
-    if gemma and _FP8_MIN_ROWS is not None and rows > _FP8_MIN_ROWS:
+    fp8 = gemma and _FP8_MIN_ROWS is not None and rows > _FP8_MIN_ROWS
+
+    def part(xs, ws):
+        if not fp8:
+            return q16(xs) @ ws.T
         if mx == "h" and _FP8_MX_H and rows <= 32:
-            xq = mx_rows(q16(x))
+            xq = mx_rows(q16(xs))
         elif mx == "x" and _FP8_MX_NORM and rows <= 32:
-            xq = mx_rows(x)
+            xq = mx_rows(xs)
         else:
-            xq = q8_rows(x)
-        y = xq @ q8_rows(w).T
+            xq = q8_rows(xs)
+        return xq @ q8_rows(ws).T
+
+    if rowpar and gemma and _FP8_MIN_ROWS is not None and _FP8_TP > 1:
+        K = x.shape[-1]
+        assert K % _FP8_TP == 0, (K, _FP8_TP)
+        ks = K // _FP8_TP
+        y = None
+        for r in range(_FP8_TP):                     # each rank's partial, summed in rank order
+            p = part(x[..., r * ks:(r + 1) * ks], w[:, r * ks:(r + 1) * ks]).astype(F32)
+            y = p if y is None else (y + p).astype(F32)
     else:
-        y = q16(x) @ w.T
+        y = part(x, w)
     if b is not None:
         y = y + b
     return y.astype(F32, copy=False)
@@ -313,14 +335,14 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     if o.shape != (B, nh, L, hd):                                       # :341-345
         raise ValueError("Size Mismatch")
     o = o.transpose(0, 2, 1, 3).reshape(B, L, -1)                       # :354-355
-    return linear(o, W[lp + "o_proj.weight"], gemma=True)                           # :356
+    return linear(o, W[lp + "o_proj.weight"], gemma=True, rowpar=True)              # :356
 
 
 def gemma_mlp(W: dict, lp: str, x: np.ndarray) -> np.ndarray:
     """GemmaMLP.forward (modeling_gemma.py:210-218)."""
     y = gelu_tanh(linear(x, W[lp + "gate_proj.weight"], gemma=True, mx="x"))
     u = linear(x, W[lp + "up_proj.weight"], gemma=True, mx="x")
-    return linear(y * u, W[lp + "down_proj.weight"], gemma=True, mx="h")
+    return linear(y * u, W[lp + "down_proj.weight"], gemma=True, mx="h", rowpar=True)
 
 
 def gemma_model(W: dict, tcfg: dict, input_embeds: np.ndarray, position_ids, mask, kv_cache,

@@ -69,6 +69,9 @@ __global__ __launch_bounds__(NW * 64) void attn_decode_wg_kernel(AttnArgs a) {
   f32x4 o[DT];
   float m, l;
   attn_decode_block32<DP, DT>(a, b, kvh, sp * a.split_keys + 32 * wave, lane, o, m, l);
+  // (the NB == 1 branch jumped straight to the LDS stores of o one instruction after the block's last MFMA, inside its
+  // write latency -- found by tests/mfma_hazard.py: the accumulators are pinned past the MFMA latency first)
+  mfma_fence(o);
   if (NB > 1) {
     const int lkv = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(a.lkv_dev ? a.lkv_dev : &pg_zero_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + a.Lkv;

@@ -106,6 +106,9 @@ __device__ __forceinline__ f32x4 mfma8s(const bf16x8& a0, const bf16x8& a1, cons
 // (16 extra wait states on top of the hazard recognizer's own, once per kernel)
 template <int N>
 __device__ __forceinline__ void mfma_fence(f32x4 (&a)[N]) {
+#ifdef PG_NO_MFMA_FENCE   // (test builds only: tests/test_host.py checks the hazard scan finds the unfenced form)
+  return;
+#endif
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_nop 7\n\ts_nop 7");
   __builtin_amdgcn_sched_barrier(0);

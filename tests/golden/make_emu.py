@@ -7,8 +7,12 @@ logits at the reference's top-64 ids, the emulated argmax and top1-top2 margin. 
 HIP fp8 path's distance to the reference by 1.5x this intrinsic distance (the bf16 tests do the same with
 oracle.bf16_operands live).
 
+--tp W (round 6): the tensor-parallel form (oracle fp8_operands(tp=W): the row-parallel o_proj / down_proj quantised
+per rank on their K slices and summed in rank order) -> <golden>_fp8emu_tp<W>.npz, the bound of the TP=W GPU test
+(tests/test_tp_gpu.py::test_tp8_pt896_fp8_batch32).
+
 Runs on the CPU in the development container (minutes per pt-896 request):
-    python tests/golden/make_emu.py [pt896wc]
+    python tests/golden/make_emu.py [pt896wc] [--tp 8]
 """
 from __future__ import annotations
 
@@ -34,14 +38,15 @@ def pixels(seed: int, size: int) -> np.ndarray:
         np.float32)
 
 
-def make(name: str, cfg: dict):
+def make(name: str, cfg: dict, tp: int = 1):
     g = dict(np.load(os.path.join(HERE, f"{name}.npz")))
     gain = float(g.get("linear_gain", 2.0))
     W = synth.generate_state_dict(cfg, gain)
     size = cfg["vision_config"]["image_size"]
-    out = {"linear_gain": np.float32(gain),
+    out = {"linear_gain": np.float32(gain), "tp": np.int32(tp),
            "mode": np.array("bf16 operands + e4m3 Gemma linears and lm_head (min_rows=0), MX decode rows (down_proj h, "
-                                   "RMSNorm-fed q|k|v, gate/up, lm_head)")}
+                            "RMSNorm-fed q|k|v, gate/up, lm_head)"
+                            + (f"; TP={tp}: o_proj / down_proj per-rank K slices, rank-order sums" if tp > 1 else ""))}
     for j, seed in enumerate(g["seeds"]):
         p = f"i{j}_"
         pv = pixels(int(seed), size)
@@ -55,7 +60,7 @@ def make(name: str, cfg: dict):
         mask = np.ones_like(ids)
         cur = ids
         vals, am, mg = [], [], []
-        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True, mx_norm=True):
+        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True, mx_norm=True, tp=tp):
             for t in range(steps):
                 lg = orc.forward(cur, pv, mask, kv, logits_rows=slice(-1, None))["logits"][0, -1]
                 vals.append(lg[top_ids[t]])
@@ -70,11 +75,17 @@ def make(name: str, cfg: dict):
         out[p + "emu_top_values"] = np.stack(vals).astype(np.float32)
         out[p + "emu_argmax"] = np.array(am, np.int64)
         out[p + "emu_margin"] = np.array(mg, np.float32)
-    np.savez_compressed(os.path.join(HERE, f"{name}_fp8emu.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, f"{name}_fp8emu" + (f"_tp{tp}" if tp > 1 else "") + ".npz"), **out)
 
 
 if __name__ == "__main__":
     import torch
     torch.set_num_threads(os.cpu_count())
-    for name in sys.argv[1:] or ["pt896wc"]:
-        make(name, {"pt896wc": configs.PT_896, "pt896": configs.PT_896, "pt448wc": configs.PT_448}[name])
+    args = sys.argv[1:]
+    tp = 1
+    if "--tp" in args:
+        i = args.index("--tp")
+        tp = int(args[i + 1])
+        del args[i:i + 2]
+    for name in args or ["pt896wc"]:
+        make(name, {"pt896wc": configs.PT_896, "pt896": configs.PT_896, "pt448wc": configs.PT_448}[name], tp)

@@ -313,3 +313,45 @@ def test_bench_refuses_world_size_other_than_gpus():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "0"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "--gpus must be >= 1" in r.stderr, r.stderr[-2000:]
+
+
+_SNIPPET = """
+0000000000001000 <k>:
+\tv_mfma_f32_16x16x32_bf16 a[0:3], v[6:9], v[10:13], 0     // 000000001000: D3B58000 02028906
+\ts_cmpk_lt_i32 s23, 0x80                                    // 000000001008: B3170080
+\ts_cbranch_scc1 3                                           // 00000000100C: BF850003 <k+0x1c>
+\ts_nop 7                                                    // 000000001010: BF800007
+\ts_nop 7                                                    // 000000001014: BF800007
+\ts_nop 7                                                    // 000000001018: BF800007
+\tv_accvgpr_read_b32 v9, a3                                  // 00000000101C: D3D84009 18000103
+\ts_endpgm                                                   // 000000001024: BF810000
+"""
+
+
+def test_mfma_hazard_scan_catches_a_branch_skipping_read():
+    """tests/mfma_hazard.py on the round-5 pattern: the fall-through path waits out the MFMA's latency (s_nops), the
+    taken branch reaches a read of its accumulator 2 wait states after it -- reported; with the branch removed, not."""
+    import mfma_hazard as H
+    bad, n = H.find_hazards(_SNIPPET)
+    assert n == 1 and len(bad) == 1 and bad[0][2].startswith("v_accvgpr_read_b32 v9, a3") and bad[0][3] == 2, bad
+    bad, _ = H.find_hazards(_SNIPPET.replace("s_cbranch_scc1 3", "s_nop 0"))
+    assert bad == [], bad
+
+
+def test_library_has_no_mfma_result_read_hazards():
+    """Every kernel of the built libpghip.so (gfx950 code objects, disassembled): no instruction on any path after a
+    v_mfma* reads its result before the MFMA's wait states have elapsed (tests/mfma_hazard.py).  Found, and fenced, in
+    round 6: attn_decode_wg_kernel's one-round branch stored the accumulators one instruction after the last MFMA."""
+    import mfma_hazard as H
+    from pghip import _lib
+    if not all(os.path.exists(os.path.join(H.LLVM, t)) for t in ("llvm-objdump", "llvm-objcopy",
+                                                                   "clang-offload-bundler")):
+        pytest.skip("ROCm LLVM tools not present")
+    cos = H.code_objects(_lib.LIB_PATH)
+    assert len(cos) >= 4
+    total = 0
+    for co in cos:
+        bad, n = H.find_hazards(H.disassemble(co))
+        total += n
+        assert bad == [], bad[:5]
+    assert total > 10000, total                      # the GEMM / GEMV / attention kernels were all scanned

@@ -115,14 +115,17 @@ def test_tp_engine_on_one_device(tmp_path, cfg, world, comm, chunk, fp8):
 
 def _check_896(res, min_checked):
     """Verdicts of tp_worker.full_size_896 (BASELINE configs[4]): bounded by the fp32 oracle run on the same e4m3 /
-    bf16 operand rounding (tests/golden/make_emu.py, <golden>_fp8emu.npz), not a flat percentage.  The single-rank
-    engine keeps the 1.5x bound; the sharded run gets 1.75x: TP reorders every o_proj / down_proj / lm_head sum (rank
-    slices, then the xGMI sum in rank order), and on this recipe that reordering alone moves the logits by 1.2-1.3x
-    the emulated distance (vs_solo_emu_ratio, measured before and after the MX decode rows)."""
+    bf16 operand rounding (tests/golden/make_emu.py), not a flat percentage.  The sharded run is bounded by the
+    emulation of the SHARDED form (<golden>_fp8emu_tp8.npz: the row-parallel o_proj / down_proj quantised per rank on
+    their K slices and summed in rank order, make_emu.py --tp 8); the single-rank engine by the single-rank emulation
+    (<golden>_fp8emu.npz).  Both at 1.5x, on every row of every block."""
     for o in res:
         assert o["xgmi_err"] == 0 and o["vision_dp"], o
-        assert o["fallbacks"] == 0, o                  # every collective went through the xGMI exchange
-        assert o["emu_ratio"] < 1.75, o                # reference top-64 within 1.75x the emulated e4m3 distance
+        assert o["emu_tp_fixture"] and o["rows_checked"] == o["B"], o
+        assert o["fallbacks"] == 0, o                  # every collective went through the xGMI kernels
+        assert o["rs_calls"] > 0 and o["chunk_allreduce_ok"], o   # prefill chunks on the reduce-scatter + all-gather
+        assert o["emu_ratio"] < 1.5, o                 # reference top-64 within 1.5x the emulated TP e4m3 distance
+        assert o["top64_rel"] < 0.3, o                 # and within 30% of the top-64 scale (non-vacuous at any margin)
         assert o["top1_bad"] == [] and o["top1_checked"] >= min_checked, o
         assert o["row_spread"] < 2e-2, o               # rows of one request agree
     r0 = res[0]
@@ -135,12 +138,12 @@ def _check_896(res, min_checked):
 def test_tp8_pt896_fp8_batch32(tmp_path):
     """BASELINE configs[4] at its own shape: PaliGemma-3B-pt-896, batch 32, fp8 Gemma linears, TP=8 (one q head, 2048
     gate/up columns, a 2048-row down slice and 32,152 vocabulary rows per rank; modeling_gemma.py:205-218, 255-259,
-    356, 523), eight ranks on one device over the xGMI exchange with cap 2^23 (every 4096-row prefill chunk and every
-    decode message fits: no collective travels over the process group).  The better-conditioned recipe's two images,
-    16 rows each (4 images per rank through the data-parallel SigLIP), prefill plus 15 teacher-forced decode steps on
-    the sharded 17..32-row fp8 GEMVs and the fp8 vocabulary-slice lm_head: every kept row within 1.5x the emulated e4m3
-    distance of the reference's top-64 logits, the reference's top-1 wherever its margin exceeds twice the step's
-    distance, and against the single-rank fp8 engine."""
+    356, 523), eight ranks on one device over the xGMI kernels (cap 2^23: every 4096-row prefill chunk runs as the
+    reduce-scatter + all-gather, every decode message as the one-shot exchange; nothing travels over the process
+    group).  The better-conditioned recipe's two images, 16 rows each (4 images per rank through the data-parallel
+    SigLIP), prefill plus 15 teacher-forced decode steps on the sharded 17..32-row fp8 GEMVs and the fp8
+    vocabulary-slice lm_head: every row within 1.5x the emulated TP e4m3 distance of the reference's top-64 logits, the
+    reference's top-1 wherever its margin exceeds twice the step's distance, and against the single-rank fp8 engine."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
     res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896", TP_B="32",
@@ -154,7 +157,7 @@ def test_tp8_pt896_fp8_batch32(tmp_path):
 def test_tp8_pt896_fp8_batch8(tmp_path):
     """The default recipe's pt-896 request (tests/golden/pt896.npz, 3 steps) at TP=8, batch 8 (one image per rank):
     the same emulation-derived bounds as the batch-32 test.  Its top1-top2 margins (0.03-0.20) lie below the e4m3
-    error, so few steps reach the top-1 check."""
+    error, so few steps reach the top-1 check; the 30% top-64 bound keeps the test from passing on bounds alone."""
     if not torch.cuda.is_available():
         pytest.skip("needs the HIP device")
     res = _launch("tp_worker.py", tmp_path, nproc=8, timeout=1100, TP_COMM="xgmi", TP_CFG="pt-896", TP_B="8",
