@@ -234,7 +234,7 @@ def tp_leg(spec, rank, world, dist, steps=2):
     B, T, fp8, sample = spec["batch"], spec["tokens"], spec.get("fp8", False), spec.get("sample", False)
     out = {"tp": tp, "config": spec["config"], "batch": B, "tokens": T, "fp8": fp8,
            "sampler": "top-p T=0.8 p=0.9 (uniforms seed 4321)" if sample else "greedy", "baseline": spec["baseline"],
-           "comm": "pg_allreduce_xgmi / pg_allgather_xgmi (decode), RCCL beyond the exchange buffer",
+           "comm": "xGMI peer-store kernels: pg_allreduce_xgmi / pg_allgather_xgmi (decode-size), pg_allreduce_xgmi_rs (prefill chunks)",
            "scaling": "strong"}
     member = rank < tp
     group = dist.new_group(list(range(tp))) if tp < world else None     # every rank calls new_group

@@ -115,12 +115,16 @@ typedef struct PgFusedArgs {
                                read), and the launch leaves fx zero (each tile's finalising workgroup clears its
                                entries)                                                                           */
   /* ABI 11 -- MX (OCP microscaling) rows for the batched fp8 decode MLP: one E8M0 scale per 32 k, no quantiser launch */
-  uint8_t* mx_out;          /* PG_EPI_BF16_GELU_MUL with PG_FP8|PG_W_FRAG, M <= 32, ksplit 1, (N/2) % 128 == 0: C is
+  uint8_t* mx_out;          /* (ABI 12: also PG_FP8 without PG_W_FRAG at M > 32 -- the prefill 128 x 128 tile -- with the
+                               scales in natural order [M][N/64], block kb of row m at m*(N/64) + kb; N % 128 == 0)
+                               PG_EPI_BF16_GELU_MUL with PG_FP8|PG_W_FRAG, M <= 32, ksplit 1, (N/2) % 128 == 0: C is
                                written as e4m3 bytes [M][ldc bytes] of h = bf16(gelu(gate)*up) / 2^e, and mx_out
                                [M][4][N/256] the E8M0 byte e + 127 of each 32-column block kb at [m][kb % 4][kb / 4],
                                e = the smallest exponent with max|h| of the block <= 448 * 2^e (0 for a zero block),
                                clamped to [-127, 127] (e4m3 RNE of h / 2^e)                                          */
-  const uint8_t* mx_in;     /* PG_FP8|PG_W_FRAG (any epilogue but F32_ADD), M <= 32, pro_mode 0: A is e4m3 [M][lda]
+  const uint8_t* mx_in;     /* (ABI 12: also PG_FP8 without PG_W_FRAG, PG_EPI_F32, M > 32 -- the prefill down projection on
+                               the 256 x 256 kernel -- with the scales in natural order [M][K/32], 4-B aligned)
+                               PG_FP8|PG_W_FRAG (any epilogue but F32_ADD), M <= 32, pro_mode 0: A is e4m3 [M][lda]
                                with mx_out's block scales [M][4][K/128] (x = q * 2^(s - 127) per 32-k block); a_scale
                                is not read.  With ss_in (rows from pg_norm_residual_mx: sums of squares per 1024
                                columns, ss_n = K / 1024 <= 4, eps) the outputs are multiplied by the row's

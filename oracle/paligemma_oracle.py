@@ -71,22 +71,24 @@ _FP8_LM_HEAD = False
 _FP8_MX_H = False
 _FP8_MX_NORM = False
 _FP8_TP = 1
+# mx_h_prefill=True (round 6, engine.MX_PREFILL): a down_proj call of MORE than 32 rows (the prefill) takes MX rows of
+# h as well -- the fp8 gate/up tile's epilogue writes e4m3 h with one E8M0 scale per 32 columns
+_FP8_MX_HP = False
 
 
 class fp8_operands:
     def __init__(self, min_rows: int = 16, lm_head: bool = False, mx_h: bool = False, mx_norm: bool = False,
-                 tp: int = 1):
-        self.min_rows, self.lm_head, self.mx_h, self.mx_norm, self.tp = min_rows, lm_head, mx_h, mx_norm, tp
+                 tp: int = 1, mx_h_prefill: bool = False):
+        self.cfg = (min_rows, lm_head, mx_h, mx_norm, tp, mx_h_prefill)
 
     def __enter__(self):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP
-        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP)
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP = (self.min_rows, self.lm_head, self.mx_h,
-                                                                          self.mx_norm, self.tp)
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP, _FP8_MX_HP
+        self._old = (_FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP, _FP8_MX_HP)
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP, _FP8_MX_HP = self.cfg
 
     def __exit__(self, *a):
-        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP
-        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP = self._old
+        global _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP, _FP8_MX_HP
+        _FP8_MIN_ROWS, _FP8_LM_HEAD, _FP8_MX_H, _FP8_MX_NORM, _FP8_TP, _FP8_MX_HP = self._old
 
 
 def mx_exp(amax: np.ndarray) -> np.ndarray:
@@ -160,7 +162,7 @@ def linear(x: np.ndarray, w: np.ndarray, b: Optional[np.ndarray] = None, gemma: 
     def part(xs, ws):
         if not fp8:
             return q16(xs) @ ws.T
-        if mx == "h" and _FP8_MX_H and rows <= 32:
+        if mx == "h" and ((_FP8_MX_H and rows <= 32) or (_FP8_MX_HP and rows > 32)):
             xq = mx_rows(q16(xs))
         elif mx == "x" and _FP8_MX_NORM and rows <= 32:
             xq = mx_rows(xs)

@@ -128,6 +128,12 @@ __device__ __forceinline__ int mx_exp(float amax) {
 __device__ __forceinline__ f32x4 mfma8(const i32x8& a, const i32x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
+// ... with the lane's E8M0 block scale for B in byte SEL of sb (MX rows in the prefill tile GEMM: one register holds
+// the scales of four row subtiles)
+template <int SEL>
+__device__ __forceinline__ f32x4 mfma8s(const i32x8& a, const i32x8& b, const f32x4& c, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, SEL, sb);
+}
 __device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {
   return __builtin_shufflevector(__builtin_bit_cast(i32x4, lo), __builtin_bit_cast(i32x4, hi), 0, 1, 2, 3, 4, 5, 6, 7);
 }

@@ -56,14 +56,22 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                         ldc >= N);
   if (epi == PG_EPI_FX_ADD) PG_REQUIRE(M <= 16 && !fp8 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N &&
                                        ((uintptr_t)C & 15) == 0 && ldc % 2 == 0);
-  if (f.mx_in) PG_REQUIRE(fp8 && frag && epi != PG_EPI_F32_ADD && M <= 32 && f.pro_mode == 0 && K % 128 == 0 &&
-                          A != nullptr && ((uintptr_t)f.mx_in & 15) == 0 &&
-                          (!f.ss_in || (f.ss_n > 0 && f.ss_n <= 4 && f.ss_ld >= f.ss_n && K == 1024 * f.ss_n)));
+  if (f.mx_in && frag) PG_REQUIRE(fp8 && epi != PG_EPI_F32_ADD && M <= 32 && f.pro_mode == 0 && K % 128 == 0 &&
+                                   A != nullptr && ((uintptr_t)f.mx_in & 15) == 0 &&
+                                   (!f.ss_in || (f.ss_n > 0 && f.ss_n <= 4 && f.ss_ld >= f.ss_n && K == 1024 * f.ss_n)));
+  // (ABI 12) the prefill tile form: MX rows [M][K] with scales [M][K/32] into the 256 x 256 fp32-slab GEMM
+  if (f.mx_in && !frag) PG_REQUIRE(fp8 && epi == PG_EPI_F32 && M > 32 && f.pro_mode == 0 && K % 128 == 0 &&
+                                   A != nullptr && ((uintptr_t)f.mx_in & 3) == 0 && !f.ss_in &&
+                                   (size_t)M * (size_t)(K / 32) < (1ull << 32) &&
+                                   (size_t)M * (size_t)lda < (1ull << 32) && (size_t)N * (size_t)ldw < (1ull << 32));
   // mx_out is written by the wide form only (gemv8x_kernel, NTW 2): launch_gemv8 takes it for GELU_MUL whenever a
   // split's x fits the LDS -- and, with MX rows in, when the split's chunk count is a compile-time 8 or 16
-  if (f.mx_out) PG_REQUIRE(fp8 && frag && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.pro_mode == 0 && !f.amax_out &&
-                           ksplit == 1 && (N / 2) % 128 == 0 && PG_GEMV8_WIDE && (K >> 7) * 128 <= 4096 &&
-                           (!f.mx_in || (K >> 7) == 8 || (K >> 7) == 16));
+  if (f.mx_out && frag) PG_REQUIRE(fp8 && epi == PG_EPI_BF16_GELU_MUL && M <= 32 && f.pro_mode == 0 && !f.amax_out &&
+                                    ksplit == 1 && (N / 2) % 128 == 0 && PG_GEMV8_WIDE && (K >> 7) * 128 <= 4096 &&
+                                    (!f.mx_in || (K >> 7) == 8 || (K >> 7) == 16));
+  // (ABI 12) the prefill tile form: e4m3 h [M][ldc bytes] + scales [M][N/64] from the 128 x 128 fp8 tile
+  if (f.mx_out && !frag) PG_REQUIRE(fp8 && epi == PG_EPI_BF16_GELU_MUL && M > 32 && f.pro_mode == 0 && !f.mx_in &&
+                                    ksplit == 1 && N % 128 == 0 && ldc >= N / 2);
   if (f.fx) PG_REQUIRE(((uintptr_t)f.fx & 15) == 0 && (f.pro_mode == 1) != (epi == PG_EPI_F32_FIN) && !fp8 &&
                        M <= 16);
   if (ksplit > 1) PG_REQUIRE(epi == PG_EPI_F32 || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD || epi == PG_EPI_FX_ADD);
@@ -86,7 +94,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   }
   if (fp8) {
     // fp8 e4m3 operands, tile GEMMs only; the kernels see byte pairs, so K / lda / ldw are halved
-    PG_REQUIRE(!frag && M > 16 && f.pro_mode == 0 && f.a_scale && f.w_scale && K % 128 == 0 && lda % 16 == 0 &&
+    PG_REQUIRE(!frag && M > 16 && f.pro_mode == 0 && (f.a_scale || f.mx_in) && f.w_scale && K % 128 == 0 && lda % 16 == 0 &&
                ldw % 16 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0);
     const int rc = pg_dispatch_tile(epi, false, true, a, lda / 2, w, ldw / 2, K / 2, ksplit, e, stream, false, n64);
     if (rc) return rc;

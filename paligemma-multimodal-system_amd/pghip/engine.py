@@ -143,6 +143,10 @@ class PaliGemmaEngine:
     # sums of squares (pg_norm_residual_mx: one workgroup per 1024 columns and row, no row-wide reduction); the GEMV applies
     # rstd to its outputs.  Replaces the norm + per-row quantiser pair
     MX_NORM = os.environ.get("PG_MX_NORM", "1") != "0"
+    # fp8 prefill MLP on MX h too (ABI 12): the 128 x 128 fp8 gate/up tile writes h as e4m3 + one E8M0 scale per 32
+    # columns (each wave owns one block per row) and the 256 x 256 fp8 down GEMM stages the block scales beside h --
+    # the row quantiser launch between them (and half of h's bytes) is gone
+    MX_PREFILL = os.environ.get("PG_MX_PREFILL", "1") != "0"
 
     AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
     # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
@@ -341,8 +345,16 @@ class PaliGemmaEngine:
                           mask_rs=(mask.stride(-2) if mask is not None else 0), **ks_t)
             n_o = self._row_parallel(attn, Lw, "o", part, T, s_o)
             xin = self._norm(x_resid, Lw["post_w"], part, n_o, xn, T)
-            self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
-            ns = self._row_parallel(h, Lw, "down", part, T, s_d)
+            if self._mx_prefill(T):
+                # MX h: e4m3 rows + block scales from the gate/up epilogue, straight into the down GEMM
+                h8 = self._buf("t_h8", (T, I), torch.uint8)
+                hs = self._buf("t_hs", (T, I // 32), torch.uint8)
+                x8, xs = xin
+                ops.gemm8(x8, xs, Lw["gu_w8"], Lw["gu_s8"], h8, epi=ops.EPI_BF16_GELU_MUL, M=T, mx_out=hs)
+                ns = self._row_parallel(("mx", h8, hs), Lw, "down", part, T, s_d)
+            else:
+                self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
+                ns = self._row_parallel(h, Lw, "down", part, T, s_d)
             if taps is not None:
                 taps.append((x_resid + part[:ns].sum(0)).clone())
         cache.length = L
@@ -366,6 +378,12 @@ class PaliGemmaEngine:
 
     def _fp8_rows(self, M: int) -> bool:
         return self.fp8 and M > 16
+
+    def _mx_prefill(self, M: int) -> bool:
+        """The fp8 prefill MLP on MX h (MX_PREFILL): the tile GEMMs (more than 32 rows) with row-major fp8 weights."""
+        L0 = self.w.tl[0]
+        return (self.MX_PREFILL and self._fp8_rows(M) and M > 32 and "gu_w8" in L0 and "down_w8" in L0
+                and self.w.inter % 128 == 0)
 
     def _mx_decode(self, B: int) -> tuple:
         """(MX h, MX norms) for a B-row decode step: the 17..32-row fp8 GEMV path with the packed fp8 weights"""
@@ -410,6 +428,9 @@ class PaliGemmaEngine:
         """One Gemma linear: bf16 (fragment-packed W) or, with fp8 weights and M > 16, the activation rows
         quantised to e4m3 (pg_quant_fp8) feeding the PG_FP8 GEMM with the per-channel weight scales."""
         w = self.w
+        if isinstance(x, tuple) and x[0] == "mx":  # MX rows (e4m3 + [M][K/32] block scales): the tile GEMM
+            return ops.gemm8(x[1], None, Lw[name + "_w8"], Lw[name + "_s8"], out, epi=epi, M=M, ksplit=ksplit, fa=fa,
+                             mx_in=x[2])
         if not isinstance(x, tuple) and self._fp8_rows(M):
             K = x.shape[1]
             x8 = self._buf(f"x8_{K}", (M, K), torch.uint8)
@@ -531,7 +552,8 @@ class PaliGemmaEngine:
         bounds = [T * c // C for c in range(C + 1)]
         works = []
         for r0, r1 in zip(bounds[:-1], bounds[1:]):
-            self._lin(x[r0:r1], Lw, name, part[0, r0:r1], ops.EPI_F32, r1 - r0, ksplit=1)
+            xc = ("mx", x[1][r0:r1], x[2][r0:r1]) if isinstance(x, tuple) else x[r0:r1]
+            self._lin(xc, Lw, name, part[0, r0:r1], ops.EPI_F32, r1 - r0, ksplit=1)
             works.append(self.comm.all_reduce_async(part[0, r0:r1]))
         for wk in works:
             wk.wait()

@@ -115,9 +115,10 @@ def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w
     """fp8 GEMM: out = epilogue((A8 . W8^T) * a_scale[m] * w_scale[n]) (PG_FP8, pg_gemm_fused).  A8, W8 are
     uint8 tensors of e4m3 bytes; `fa` (fused_args) carries the RoPE/KV epilogue arguments for EPI_QKV_ROPE.
     frag: W8 is fp8 fragment-packed (weights.frag_pack8) -> the weight-streaming fp8 GEMV, M <= 32.
-    MX rows (frag only): mx_in = A8's E8M0 block scales [M][4][K/128] (EPI_F32; a_scale None), mx_out = the
-    scales a gelu*up launch writes beside its e4m3 h (out uint8 [M][N/2]); ss_in (with mx_in, rows from
-    norm_residual_mx): the outputs are multiplied by each row's RMSNorm rstd."""
+    MX rows: mx_in = A8's E8M0 block scales (EPI_F32; a_scale None), mx_out = the scales a gelu*up launch writes
+    beside its e4m3 h (out uint8 [M][N/2]).  Layout: frag (decode GEMV) [M][4][K/128]; tile (M > 32, the prefill, ABI
+    12) [M][K/32], block b of row m at m*K/32 + b.  ss_in (frag, with mx_in, rows from norm_residual_mx): the outputs
+    are multiplied by each row's RMSNorm rstd."""
     for t, n in ((A8, "A8"), (W8, "W8")):
         if t.dtype != torch.uint8 or not t.is_cuda or t.stride(1) != 1:
             raise ValueError(f"pghip.gemm8: {n} must be a row-major uint8 (e4m3) HIP tensor")
@@ -132,9 +133,10 @@ def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w
     for t, n, numel in ((mx_in, "mx_in", M * K // 32), (mx_out, "mx_out", M * N // 64)):
         if t is None:
             continue
-        if not frag or t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous() or t.numel() < numel:
+        if (t.dtype != torch.uint8 or not t.is_cuda or not t.is_contiguous() or t.numel() < numel
+                or (not frag and M <= 32)):
             raise ValueError(f"pghip.gemm8: {n} must be a contiguous uint8 HIP tensor of >= {numel} E8M0 scales "
-                             "(fragment-packed W8 only)")
+                             "(the fp8 GEMV, or the tile GEMM at M > 32)")
         setattr(fa, n, t.data_ptr())
     if ss_in is not None:
         _chk(ss_in, torch.float32, "ss_in")
@@ -149,7 +151,7 @@ def gemm8(A8: torch.Tensor, a_scale: Optional[torch.Tensor], W8: torch.Tensor, w
         _lib.call("pg_gemm_fused", _p(A8), A8.stride(0), _p(W8), W8.stride(0), _p(bias), _p(out), ldc, M, N, K,
                   e | EPI_FP8 | W_FRAG, ksplit, _lib.C.byref(fa), _s())
         return out
-    s = finalize_split(M, N, K // 2) if ksplit == 1 and e in _FIN_EPIS else 1
+    s = finalize_split(M, N, K // 2) if ksplit == 1 and e in _FIN_EPIS and mx_out is None else 1
     if s > 1:   # small M: fp32 slabs, then the epilogue (scales already applied inside the slabs)
         part = torch.empty(s, M, N, dtype=torch.float32, device=out.device)
         _lib.call("pg_gemm_fused", _p(A8), A8.stride(0), _p(W8), W8.stride(0), _p(bias), _p(part), N, M, N, K,

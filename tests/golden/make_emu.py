@@ -45,7 +45,7 @@ def make(name: str, cfg: dict, tp: int = 1):
     size = cfg["vision_config"]["image_size"]
     out = {"linear_gain": np.float32(gain), "tp": np.int32(tp),
            "mode": np.array("bf16 operands + e4m3 Gemma linears and lm_head (min_rows=0), MX decode rows (down_proj h, "
-                            "RMSNorm-fed q|k|v, gate/up, lm_head)"
+                            "RMSNorm-fed q|k|v, gate/up, lm_head), MX prefill h (round 6)"
                             + (f"; TP={tp}: o_proj / down_proj per-rank K slices, rank-order sums" if tp > 1 else ""))}
     for j, seed in enumerate(g["seeds"]):
         p = f"i{j}_"
@@ -60,7 +60,8 @@ def make(name: str, cfg: dict, tp: int = 1):
         mask = np.ones_like(ids)
         cur = ids
         vals, am, mg = [], [], []
-        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True, mx_norm=True, tp=tp):
+        with O.bf16_operands(), O.fp8_operands(min_rows=0, lm_head=True, mx_h=True, mx_norm=True, tp=tp,
+                                                       mx_h_prefill=True):
             for t in range(steps):
                 lg = orc.forward(cur, pv, mask, kv, logits_rows=slice(-1, None))["logits"][0, -1]
                 vals.append(lg[top_ids[t]])

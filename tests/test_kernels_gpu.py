@@ -1027,6 +1027,42 @@ def test_mx_h_gate_up_and_down(M, I, H, ks):
         assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
 
 
+@pytest.mark.parametrize("M,I,H,ks", [(300, 1024, 512, 1), (33, 2048, 2048, 2), (1100, 16384, 2048, 3),
+                                      (4200, 4096, 1024, 1)])
+def test_mx_h_prefill_tiles(M, I, H, ks):
+    """The fp8 prefill MLP on MX rows (ABI 12, engine.MX_PREFILL): the 128 x 128 fp8 gate/up tile writes h as e4m3
+    with one E8M0 scale per 32 columns, natural layout [M][I/32] -- bit-identical to the torch MX rule on the bf16
+    gelu*up tile's h (one e4m3 step allowed where the two launches' bf16 h differ by an ulp) -- and the 256 x 256 fp8
+    fp32-slab GEMM reading those block scales beside the rows (mx_in) equals a float64 matmul of the dequantised
+    operands up to fp32 summation order; also on scales spread over 2^-10 .. 2^10 and with split-K slabs."""
+    from pghip import ops
+    from pghip.weights import quant_rows_fp8
+    x = rnd(M, H, seed=91)
+    Wgu, Wd = rnd(2 * I, H, scale=1 / math.sqrt(H), seed=92), rnd(H, I, scale=1 / math.sqrt(I), seed=93)
+    x8, xs = ops.quant_fp8(x)
+    gu8, gus = quant_rows_fp8(Wgu)
+    d8, ds = quant_rows_fp8(Wd)
+    h0 = torch.empty(M, I, dtype=torch.bfloat16, device="cuda")
+    ops.gemm8(x8, xs, gu8, gus, h0, epi=ops.EPI_BF16_GELU_MUL)
+    h8 = torch.full((M, I), 0x55, dtype=torch.uint8, device="cuda")
+    hs = torch.full((M, I // 32), 0x55, dtype=torch.uint8, device="cuda")
+    ops.gemm8(x8, xs, gu8, gus, h8, epi=ops.EPI_BF16_GELU_MUL, mx_out=hs)
+    q_ref, s_ref = _mx_quant(h0.float())
+    s_ref = s_ref.view(M, 4, I // 128).permute(0, 2, 1).reshape(M, I // 32)      # natural [M][I/32] order
+    same_s = (hs == s_ref).float().mean().item()
+    same_q = (h8 == q_ref).float().mean().item()
+    assert same_s > 0.999 and same_q > 0.999, (same_s, same_q)
+    deq = (h8.view(torch.float8_e4m3fn).float().view(M, I // 32, 32) * torch.exp2(hs.float() - 127)[..., None])
+    assert err(deq.view(M, I), h0.float()) < 0.07                      # e4m3: 3 mantissa bits per block
+    for scales, tol in ((hs, 1e-4), (torch.randint(117, 138, (M, I // 32), dtype=torch.uint8, device="cuda"), 3e-4)):
+        dq = (h8.view(torch.float8_e4m3fn).double().view(M, I // 32, 32) *
+              torch.exp2(scales.double() - 127)[..., None]).view(M, I)
+        ref = (dq @ _deq(d8, ds).double().t()).float()
+        part = torch.empty(ks, M, H, dtype=torch.float32, device="cuda")
+        ops.gemm8(h8, None, d8, ds, part, epi=ops.EPI_F32, ksplit=ks, mx_in=scales)
+        assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
+
+
 @pytest.mark.parametrize("M,H,nsplit,I", [(32, 2048, 8, 16384), (17, 2048, 2, 4096), (24, 3072, 0, 1024),
                                           (32, 2048, 11, 2048), (20, 1024, 1, 2048)])
 def test_mx_norm_rows_and_rstd_consumers(M, H, nsplit, I):

@@ -103,7 +103,7 @@ def tiny(rank, world, name):
         out[f"prefill_err_vs_solo_b{B}"] = err(lg[0].cpu().numpy(), lg[1].cpu().numpy())
         # the model's own sensitivity to the HIP path's operand rounding: the fp32 oracle with bf16 operands (and
         # e4m3 Gemma linears of more than 16 rows for fp8) against the reference's logits
-        with O.bf16_operands(), (O.fp8_operands() if fp8 else contextlib.nullcontext()):
+        with O.bf16_operands(), (O.fp8_operands(mx_h_prefill=True) if fp8 else contextlib.nullcontext()):
             lo = O.PaliGemmaOracle(ocfg_, W, recompute_vision=False).forward(
                 g[p + "input_ids"], g[p + "pixel_values"], np.ones_like(g[p + "input_ids"]), O.KVCache())["logits"]
         out[f"intrinsic_b{B}"] = err(lo.reshape(Bv * L, -1), g[p + "logits"].reshape(Bv * L, -1))
@@ -163,7 +163,7 @@ def tiny(rank, world, name):
         kve = [O.KVCache() for _ in range(Bd)]
 
         def emu_fwd(*a, **k):
-            with O.bf16_operands(), O.fp8_operands(min_rows=0):
+            with O.bf16_operands(), O.fp8_operands(min_rows=0, mx_h_prefill=True):
                 return emu.forward(*a, **k)
         ref = [orc.forward(ids_b[b:b + 1], pxb[b:b + 1], amb[b:b + 1], kvs[b], logits_rows=slice(-1, None))
                ["logits"][0, -1] for b in range(Bd)]
