@@ -129,9 +129,14 @@ __device__ __forceinline__ f32x4 mfma8(const i32x8& a, const i32x8& b, const f32
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 // ... with the lane's E8M0 block scale for B in byte SEL of sb (MX rows in the prefill tile GEMM: one register holds
-// the scales of four row subtiles)
+// the scales of the wave's row subtiles)
 template <int SEL>
-__device__ __forceinline__ f32x4 mfma8s(const i32x8& a, const i32x8& b, const f32x4& c, int sb) {
+__device__ __forceinline__ f32x4 mfma8s_sel(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0, const bf16x8& b1,
+                                            const f32x4& c, int sb) {
+  const i32x4 x0 = __builtin_bit_cast(i32x4, a0), x1 = __builtin_bit_cast(i32x4, a1);
+  const i32x4 y0 = __builtin_bit_cast(i32x4, b0), y1 = __builtin_bit_cast(i32x4, b1);
+  const i32x8 a = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const i32x8 b = __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, SEL, sb);
 }
 __device__ __forceinline__ i32x8 cat8(const bf16x8& lo, const bf16x8& hi) {

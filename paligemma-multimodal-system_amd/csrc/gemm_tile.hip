@@ -91,15 +91,26 @@ __device__ __forceinline__ void wait_vm(int n) {   // s_waitcnt vmcnt(n), n in [
 // KSUB = 2: a stage holds two 64-k sub-tiles (K % 128 == 0), one barrier / vmcnt wait per 128 k: half the
 // per-k-step synchronisation of the latency-bound small-M tiles.
 // WNT: the W pieces are staged non-temporal (aux 2): for grids where each W tile is read by ONE workgroup (PG_TILE_M1)
+// MXA (fp8, ABI 12): A rows are MX (OCP microscaling) e4m3 with one E8M0 scale per 32 k, PgFusedArgs.mx_in [M][K/32]
+// (the prefill gate/up epilogue's h, into the down projection): each stage also brings its BM rows' 4 block scales
+// of the k-step into LDS -- one byte per lane of every wave (zero-extended into the lane's dword slot), stored
+// transposed so that lane (r, g) of wave row wm reads its NI row subtiles' block-g scales with one 8-byte read -- and
+// the MFMA of subtile i takes byte i of the packed pair (op_sel).  The MFMA
+// reads block b's scale from lane group b: with the (g, 4 + g) chunk pairs below, lane group b holds block b's k
+// ranges in the hardware's k order (k = 64 half + 16 g + byte), so MX block b is hardware block b.
 template <int EPI, int BM, int STAGES, bool FRAG, bool F8 = false, int WAVES = 4, int BN = TBN, int KSUB = 1,
-          bool WNT = false>
+          bool WNT = false, bool MXA = false>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __restrict__ A, int lda,
                                                                const bf16_t* __restrict__ W, int ldw, int K,
                                                                int kchunk, int tiles_m, int tiles_n, EpiArgs e) {
   constexpr int A_BYTES = BM * TBK * 2;
   static_assert(BN == TBN || (BN == 64 && BM == 64 && WAVES == 4), "BN 64: 64-row tiles of 4 waves only");
+  static_assert(!MXA || (F8 && KSUB == 1 && BM * 4 == WAVES * 64), "MX rows: fp8, one byte per lane per stage");
   constexpr int W_BYTES = BN * TBK * 2;
-  constexpr int SUB_BYTES = A_BYTES + W_BYTES;
+  // the stage's block scales (4 per row per 128-k step), one per dword: LDS DMA of a byte zero-extends it into the
+  // lane's dword slot
+  constexpr int S_BYTES = MXA ? BM * 4 * 4 : 0;
+  constexpr int SUB_BYTES = A_BYTES + W_BYTES + S_BYTES;
   constexpr int STAGE_BYTES = KSUB * SUB_BYTES;
   constexpr int WN = BN == 64 ? 2 : (WAVES == 4 ? (BM == 64 ? 4 : 2) : (WAVES == 8 ? (BM == 64 ? 4 : 2) : 2));
   constexpr int WM = WAVES / WN;                   // waves along M
@@ -131,7 +142,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
   const int m0 = tm * BM, n0 = tn * BN;
   // glds pieces this wave issues per stage (wave-uniform): its vmcnt step per younger stage in flight; A pieces of
   // padding rows only (the last row tile: M = 264 in a 288-row tile) are not loaded
-  const int P = KSUB * (stage_pieces<BM, NWA, true>(m0, e.M, wave) + stage_pieces<BN, NWW, false>(n0, e.N, wave));
+  const int P = KSUB * (stage_pieces<BM, NWA, true>(m0, e.M, wave) + stage_pieces<BN, NWW, false>(n0, e.N, wave)) +
+                (MXA ? 1 : 0);
 
   const int z = blockIdx.z;
   const int kbeg = z * kchunk;
@@ -152,6 +164,17 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
       const int k0 = kbeg + (kt * KSUB + u) * TBK;
       stage_tile<BM, false, NWA, 0, true>(A, lda, m0, e.M, k0, st + u * SUB_BYTES, wave, lane);
       stage_tile<BN, FRAG, NWW, WNT ? 2 : 0>(W, ldw, n0, e.N, k0, st + u * SUB_BYTES + A_BYTES, wave, lane);
+      if constexpr (MXA) {
+        // slot ((wm * 16 + r) * 4 + g) * NI + i = block g of tile row wm * (BM / WM) + i * 16 + r (transposed)
+        const int idx = wave * 64 + lane;
+        const int i = idx % NI, g = (idx / NI) & 3, r = (idx / (NI * 4)) & 15, wmr = idx / (NI * 64);
+        const int gr = min(m0 + wmr * (BM / WM) + i * 16 + r, e.M - 1);
+        // (uniform base + 32-bit offset: the scales are M * K / 16 bytes, host-checked < 4 GiB; K counts byte pairs)
+        const char* src = (const char*)e.f.mx_in + (uint32_t)((unsigned)gr * (unsigned)(K >> 4) +
+                                                              (unsigned)(k0 >> 6) * 4u + (unsigned)g);
+        __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(st + A_BYTES + W_BYTES + wave * 256), 1, 0,
+                                         0);
+      }
     }
   };
 #pragma unroll
@@ -182,10 +205,21 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 #pragma unroll
         for (int j = 0; j < NJ; ++j) fw[j][s] = lds_frag(tW, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
       }
+      if constexpr (MXA) {
+        static_assert(NI == 2, "MX rows: two row subtiles per wave (one 16-bit scale word per lane)");
+        const u32x2 sv = *(const u32x2*)(tW + W_BYTES + ((wm * 16 + (lane & 15)) * 4 + (lane >> 4)) * NI * 4);
+        const int scp = (int)(sv[0] | (sv[1] << 8));    // subtile 0's scale in byte 0, subtile 1's in byte 1
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          acc[0][j] = mfma8s_sel<0>(fw[j][0], fw[j][1], fa[0][0], fa[0][1], acc[0][j], scp);
+          acc[1][j] = mfma8s_sel<1>(fw[j][0], fw[j][1], fa[1][0], fa[1][1], acc[1][j], scp);
+        }
+      } else {
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = mfma8(fw[j][0], fw[j][1], fa[i][0], fa[i][1], acc[i][j]);
+      }
     } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -269,18 +303,12 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 // B0 of t+1 in phase 0), so 3 half-tiles (6 loads per thread) stay in flight across the raw s_barrier that
 // ends every phase; the single counted wait (vmcnt 6) sits in phase 3 and the tile it retires is read
 // from phase 0 of the next tile on (MI355X guide: 256^2 8-phase template, counted vmcnt, T1/T2/T5).
-// MXA (fp8, ABI 12): A rows are MX (OCP microscaling) e4m3 with one E8M0 scale per 32 k, PgFusedArgs.mx_in [M][K/32]
-// (the prefill gate/up epilogue's h): each A-half stage also brings its 128 rows' 4 scales of the k-tile into LDS
-// (waves 0 and 1, one dword per row), lane group g reads the 32 contiguous k of MX block g (chunks 2g, 2g + 1, W alike)
-// and the MFMA takes the lane's block scale for its A row.
-template <int EPI, bool FRAG, bool F8 = false, bool MXA = false>
+template <int EPI, bool FRAG, bool F8 = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__ A, int lda,
                                                       const bf16_t* __restrict__ W, int ldw, int K,
                                                       int ktiles_per_split, int tiles_m, int tiles_n, EpiArgs e) {
   constexpr int HALF = 16384;
-  static_assert(!MXA || F8, "MX rows are fp8");
-  __shared__ __attribute__((aligned(1024))) char smem[8 * HALF + (MXA ? 4 * 512 : 0)];
-  char* const sscale = smem + 8 * HALF;                 // MXA: [2 buffers][2 A halves][128 rows] u32 (4 E8M0 bytes)
+  __shared__ __attribute__((aligned(1024))) char smem[8 * HALF];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -329,22 +357,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(dst + blk * 1024), 16, 0, 0);
     }
-    if constexpr (MXA) {
-      // the A half's 128 rows' scales of this k-tile (4 blocks of 32 fp8 k = one dword per row): waves 0 / 1 take
-      // half-image rows [64 wave, +64)
-      if (h < 2 && __builtin_amdgcn_readfirstlane(wave) < 2) {
-        const int r = wave * 64 + lane;
-        const int gr = min(m0 + (r >> 6) * 128 + h * 64 + (r & 63), e.M - 1);
-        // (uniform base + 32-bit offset, as the operands: the scales are M * K / 16 bytes, host-checked < 4 GiB)
-        const char* src = (const char*)e.f.mx_in + (uint32_t)((unsigned)gr * (unsigned)(K >> 4) +
-                                                              (unsigned)(kt0 + kt) * 4u);
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (LDS_AS void*)(sscale + (((kt & 1) * 2 + h) * 128 + wave * 64) * 4), 4, 0, 0);
-      }
-    }
   };
-  // counted vmcnt of three half-tiles in flight: the scale dword is a third load of waves 0 / 1 on A halves
-  const int vm_inflight = (MXA && __builtin_amdgcn_readfirstlane(wave) < 2) ? 8 : 6;
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -358,14 +371,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   FA fa0, fa1;
   FB fb0, fb1;
 
-  // fp8 chunk pair of lane group g: (g, 4 + g), or with MX rows the 32 contiguous k of block g (2g, 2g + 1)
-  const int ck0 = MXA ? 2 * (lane >> 4) : (lane >> 4), ck1 = MXA ? ck0 + 1 : 4 + (lane >> 4);
   auto read_a = [&](const char* img, auto& fa) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = wr * 64 + i * 16 + (lane & 15);
       if constexpr (F8) {
-        fa[i] = cat8(lds_frag(img, row, ck0), lds_frag(img, row, ck1));
+        fa[i] = cat8(lds_frag(img, row, lane >> 4), lds_frag(img, row, 4 + (lane >> 4)));
       } else {
 #pragma unroll
         for (int s = 0; s < 2; ++s) fa[i][s] = lds_frag(img, row, s * 4 + (lane >> 4));
@@ -377,34 +388,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     for (int j = 0; j < 2; ++j) {
       const int row = wc * 32 + j * 16 + (lane & 15);
       if constexpr (F8) {
-        fb[j] = cat8(lds_frag(img, row, ck0), lds_frag(img, row, ck1));
+        fb[j] = cat8(lds_frag(img, row, lane >> 4), lds_frag(img, row, 4 + (lane >> 4)));
       } else {
 #pragma unroll
         for (int s = 0; s < 2; ++s) fb[j][s] = lds_frag(img, row, s * 4 + (lane >> 4));
       }
     }
   };
-  // MXA: the lane's A-row block scales of the current k-tile, per A half (read with the half's fragments), packed one
-  // byte per row subtile i into one register; the MFMA of subtile i selects byte i (op_sel)
-  int scp = 0;
-  auto read_scales = [&](int t, int rh) {
-    if constexpr (MXA) {
-      const uint8_t* sp = (const uint8_t*)sscale + (((t & 1) * 2 + rh) * 128 + wr * 64 + (lane & 15)) * 4 + (lane >> 4);
-      scp = (int)((uint32_t)sp[0] | ((uint32_t)sp[16 * 4] << 8) | ((uint32_t)sp[32 * 4] << 16) |
-                  ((uint32_t)sp[48 * 4] << 24));
-    }
-  };
   auto mma = [&](int rh, int ch, const auto& fa, const auto& fb) {
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (MXA) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[rh * 4 + 0][ch * 2 + j] = mfma8s<0>(fb[j], fa[0], acc[rh * 4 + 0][ch * 2 + j], scp);
-        acc[rh * 4 + 1][ch * 2 + j] = mfma8s<1>(fb[j], fa[1], acc[rh * 4 + 1][ch * 2 + j], scp);
-        acc[rh * 4 + 2][ch * 2 + j] = mfma8s<2>(fb[j], fa[2], acc[rh * 4 + 2][ch * 2 + j], scp);
-        acc[rh * 4 + 3][ch * 2 + j] = mfma8s<3>(fb[j], fa[3], acc[rh * 4 + 3][ch * 2 + j], scp);
-      }
-    } else if constexpr (F8) {
+    if constexpr (F8) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -432,7 +425,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     stage(0, 1);
     stage(3, 1);
     stage(1, 1);
-    wait_vm_n(vm_inflight);
+    wait_vm(6);
   } else {
     wait_vm(0);
   }
@@ -503,7 +496,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     } else {
     // phase 0: quadrant (rows 0-63, cols 0-31) from A0, B0; restage B0 of tile t+1
     read_a(buf, fa0);
-    read_scales(t, 0);
     read_b(buf + 2 * HALF, fb0);
     if (t + 1 < nk) stage(2, t + 1);
     mma(0, 0, fa0, fb0);
@@ -515,7 +507,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     __builtin_amdgcn_s_barrier();
     // phase 2: (rows 64-127, cols 32-63) A1, B regs kept; restage B1 of tile t+2
     read_a(buf + 1 * HALF, fa0);
-    read_scales(t, 1);
     if (t + 2 < nk) stage(3, t + 2);
     mma(1, 1, fa0, fb0);
     __builtin_amdgcn_s_barrier();
@@ -524,7 +515,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
     if (t + 2 < nk) stage(1, t + 2);
     mma(1, 0, fa0, fb0);
     }
-    if (t + 2 < nk) wait_vm_n(vm_inflight); else wait_vm(0);
+    if (t + 2 < nk) wait_vm(6); else wait_vm(0);
     __builtin_amdgcn_s_barrier();
   }
 
@@ -684,29 +675,26 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
       return;
     }
   }
+  if constexpr (F8 && (EPI == PG_EPI_F32 || EPI == PG_EPI_BF16_GELU_MUL)) {
+    if (e.f.mx_in || e.f.mx_out) {
+      // (ABI 12) MX rows in (the prefill down projection) / MX h out (the prefill gate/up): the 128 x 128 fp8 tile, whose
+      // waves own 32 rows x 64 W rows -- one 32-column h block per row (out), two row subtiles of scales (in)
+      const int tiles_n = (e.N + TBN - 1) / TBN, tiles_m = (e.M + 127) / 128;
+      const int kchunk = ((K / TBK + ksplit - 1) / ksplit) * TBK;
+      if (e.f.mx_in)
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, PG_T128_STAGES_F8, FRAG, true, PG_TILE_W128, TBN, 1, false, true>),
+                           dim3(tiles_m * tiles_n, 1, ksplit), dim3(64 * PG_TILE_W128), 0, st, A, lda, W, ldw, K,
+                           kchunk, tiles_m, tiles_n, e);
+      else
+        hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, PG_T128_STAGES_F8, FRAG, true, PG_TILE_W128>),
+                           dim3(tiles_m * tiles_n, 1, ksplit), dim3(64 * PG_TILE_W128), 0, st, A, lda, W, ldw, K,
+                           kchunk, tiles_m, tiles_n, e);
+      return;
+    }
+  }
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
   // (fp8 on the 256 x 256 kernel addresses its operands by 32-bit byte offsets: both must be < 4 GiB)
   const bool off32 = (size_t)e.M * lda * 2 < (1ull << 32) && (size_t)e.N * ldw * 2 < (1ull << 32);
-  if constexpr (F8 && EPI == PG_EPI_F32) {
-    if (e.f.mx_in) {
-      // (ABI 12) MX rows in (the prefill down projection on the gate/up epilogue's MX h): the 256 x 256 kernel
-      // stages the A block scales beside A (host-checked: off32, ksplit as the slab count)
-      const int kts = (K / 64 + ksplit - 1) / ksplit;
-      hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG, true, true>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W,
-                         ldw, K, kts, (e.M + 255) / 256, (e.N + 255) / 256, e);
-      return;
-    }
-  }
-  if constexpr (F8 && EPI == PG_EPI_BF16_GELU_MUL) {
-    if (e.f.mx_out) {
-      // (ABI 12) MX h out: the 128 x 128 tile, whose waves each own one 32-column h block per row
-      const int tiles_n = (e.N + TBN - 1) / TBN, tiles_m = (e.M + 127) / 128;
-      hipLaunchKernelGGL((gemm_tile_kernel<EPI, 128, PG_T128_STAGES_F8, FRAG, true, PG_TILE_W128>),
-                         dim3(tiles_m * tiles_n, 1, 1), dim3(64 * PG_TILE_W128), 0, st, A, lda, W, ldw, K,
-                         (K / TBK) * TBK, tiles_m, tiles_n, e);
-      return;
-    }
-  }
   constexpr bool g256 = !F8 || PG_F8_G256 == 2 || (PG_F8_G256 == 1 && EPI == PG_EPI_F32);
   if (g256 && (!F8 || off32) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;

@@ -1054,13 +1054,15 @@ def test_mx_h_prefill_tiles(M, I, H, ks):
     assert same_s > 0.999 and same_q > 0.999, (same_s, same_q)
     deq = (h8.view(torch.float8_e4m3fn).float().view(M, I // 32, 32) * torch.exp2(hs.float() - 127)[..., None])
     assert err(deq.view(M, I), h0.float()) < 0.07                      # e4m3: 3 mantissa bits per block
-    for scales, tol in ((hs, 1e-4), (torch.randint(117, 138, (M, I // 32), dtype=torch.uint8, device="cuda"), 3e-4)):
+    unit = torch.full((M, I // 32), 127, dtype=torch.uint8, device="cuda")
+    for scales, tol in ((unit, 1e-4), (hs, 1e-4),
+                        (torch.randint(117, 138, (M, I // 32), dtype=torch.uint8, device="cuda"), 3e-4)):
         dq = (h8.view(torch.float8_e4m3fn).double().view(M, I // 32, 32) *
               torch.exp2(scales.double() - 127)[..., None]).view(M, I)
         ref = (dq @ _deq(d8, ds).double().t()).float()
         part = torch.empty(ks, M, H, dtype=torch.float32, device="cuda")
         ops.gemm8(h8, None, d8, ds, part, epi=ops.EPI_F32, ksplit=ks, mx_in=scales)
-        assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol)
+        assert err(part.sum(0), ref) < tol, (float(err(part.sum(0), ref)), tol, int((scales == 127).all()))
 
 
 @pytest.mark.parametrize("M,H,nsplit,I", [(32, 2048, 8, 16384), (17, 2048, 2, 4096), (24, 3072, 0, 1024),
