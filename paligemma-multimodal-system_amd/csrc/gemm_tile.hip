@@ -597,9 +597,12 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
                              // gate/up 10.1 -> 14.6 / 14.3 ms)
 #endif
 #ifndef PG_F8_G256
-// fp8 GEMMs on the 256x256 kernel: 0 never, 1 the fp32-slab epilogue only (pt-896 x32 o + down 115.7 -> 102.5 ms per
-// prefill), 2 every epilogue (gate/up 182 -> 211 ms and q|k|v 21 -> 48 ms: those instances still spill)
-#define PG_F8_G256 1
+// fp8 GEMMs on the 256x256 kernel: 0 never, 1 the fp32-slab epilogue only (round 4: pt-896 x32 o + down 115.7 -> 102.5
+// ms per prefill), 2 every epilogue (gate/up 182 -> 211 ms and q|k|v 21 -> 48 ms: those instances still spill).
+// Round 6: with the down projection on MX rows (the 128 x 128 tile, 5.3 ms vs 6.3 on the 256 kernel), the o_proj
+// alone is faster on the 128 x 128 tile too: pt-896 x32 prefill 698.9 / 699.7 -> 695.3 / 696.5 ms
+// (profiles/r06_fp8_prefill_ab.jsonl), so 0
+#define PG_F8_G256 0
 #endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU
