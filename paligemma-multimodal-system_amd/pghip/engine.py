@@ -382,8 +382,10 @@ class PaliGemmaEngine:
     def _mx_prefill(self, M: int) -> bool:
         """The fp8 prefill MLP on MX h (MX_PREFILL): the tile GEMMs (more than 32 rows) with row-major fp8 weights."""
         L0 = self.w.tl[0]
+        # (under TP the down projection may run as row chunks (_row_parallel): each must keep > 32 rows)
+        chunks_ok = self.tp == 1 or M < 2 * self.AR_CHUNK_ROWS or self.AR_CHUNK_ROWS >= 64
         return (self.MX_PREFILL and self._fp8_rows(M) and M > 32 and "gu_w8" in L0 and "down_w8" in L0
-                and self.w.inter % 128 == 0)
+                and self.w.inter % 128 == 0 and chunks_ok)
 
     def _mx_decode(self, B: int) -> tuple:
         """(MX h, MX norms) for a B-row decode step: the 17..32-row fp8 GEMV path with the packed fp8 weights"""

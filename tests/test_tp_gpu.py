@@ -25,10 +25,12 @@ def _port():
 
 
 def _launch(worker, tmp_path, nproc=2, timeout=600, **env):
-    # ranks sharing ONE device: at most 2 hardware queues per rank, so the 8 ranks' queues all stay mapped at once (an
-    # oversubscribed queue set is time-sliced, and a rank whose queue is not mapped cannot reach an exchange its peers
-    # spin in: measured as an occasional 20 s xGMI timeout at 8 ranks x 4 queues; a real node has a device per rank)
-    env = dict(os.environ, TP_OUT=str(tmp_path), GPU_MAX_HW_QUEUES="2", **env)
+    # ranks sharing ONE device: at most 2 hardware queues per rank (TP_HW_QUEUES), so the 8 ranks' queues -- and this
+    # pytest process's own, which holds a context from the earlier tests -- all stay mapped at once.  An oversubscribed
+    # queue set is time-sliced, and a rank whose queue is not mapped cannot reach an exchange its peers spin in (an
+    # occasional 20 s xGMI timeout at 8 ranks x 4 queues in round 5; DESIGN §6 has the analysis).  A real node has a
+    # device per rank, at most 4 queues each.
+    env = dict(os.environ, TP_OUT=str(tmp_path), GPU_MAX_HW_QUEUES=os.environ.get("TP_HW_QUEUES", "2"), **env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", worker)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
