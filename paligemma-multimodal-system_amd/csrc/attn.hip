@@ -25,6 +25,18 @@
 #ifndef PG_FA_W12
 #define PG_FA_W12 1       // prefill, head_dim 256: 12-wave workgroups when they fill the one-per-CU rounds better
 #endif
+#ifndef PG_FA_W8R2
+#define PG_FA_W8R2 1      // head_dim 256: 8 waves x 2 row groups (256 rows per workgroup) on 32-key blocks
+#endif
+#ifndef PG_FA_W8R2_NST
+#define PG_FA_W8R2_NST 2  // (4 / 5 stages measured 4-5% slower at pt-896 x32)
+#endif
+#ifndef PG_FA_W8R2_HOIST
+#define PG_FA_W8R2_HOIST 4
+#endif
+#ifndef PG_FA_PRIO
+#define PG_FA_PRIO 0
+#endif
 #ifndef PG_COMBINE_PF
 #define PG_COMBINE_PF 12  // split-KV merge: O partials of the first 12 splits per thread loaded up front
 #endif
@@ -783,6 +795,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   constexpr int VIMG = DT * 16 * VROW;
   constexpr int STAGE = KIMG + VIMG;
   constexpr int KINS = KIMG / 1024, VINS = VIMG / 1024;   // glds wave-instructions per block
+  constexpr int FA_HOIST = (DP == 256 && WAVES == 8 && RPW == 2) ? PG_FA_W8R2_HOIST : 0;
   static_assert(KIMG % 1024 == 0 && VIMG % 1024 == 0 && NST * STAGE <= 163840, "stage images");
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
@@ -858,6 +871,8 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
   for (int sb = 0; sb < NST - 1; ++sb)
     if (sb < nblk) stage(kb0 + sb * KB, sb);
+  // static priority for the second-dispatched half of a 2-wave-per-SIMD workgroup (tuning knob)
+  if constexpr (PG_FA_PRIO) if (WAVES >= 8 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
   for (int ib = 0; ib < nblk; ++ib) {
     const int kb = kb0 + ib * KB;
     // block ib has landed once at most (blocks issued after it) * P of this wave's pieces are outstanding
@@ -873,13 +888,17 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) sc[i][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s) {
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt) {
         const bf16x8 kf = *(const bf16x8*)(kimg + ((kt * NCH + 4 * s + g) * 16 + c) * 16);
 #pragma unroll
         for (int i = 0; i < RPW; ++i) sc[i][kt] = mfma16(kf, qf[i][s], sc[i][kt]);
       }
+      // (256 rows of head_dim 256 per 8-wave workgroup: at most FA_HOIST fragment reads ahead, or the
+      // hoisted reads push the wave past its 256 registers)
+      if constexpr (FA_HOIST > 0) if ((s + 1) % (FA_HOIST / NKT) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
     // lane holds S[key = kb + 32 (kt / 2) + 8g + 4 (kt % 2) + j][q = c] of each row group
     bf16x8 pf[RPW][KB / 32];
 #pragma unroll
@@ -945,6 +964,7 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
         const bf16x8 vf = *(const bf16x8*)(vr + ((4 * h + g) ^ sw) * 16);   // keys 32h + 8g .. + 7
 #pragma unroll
         for (int i = 0; i < RPW; ++i) o[i][tt] = mfma16(vf, pf[i][h], o[i][tt]);
+        if constexpr (FA_HOIST > 0) if ((tt + 1) % FA_HOIST == 0) __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -1107,6 +1127,21 @@ struct FaDeep {
   static constexpr int NST = N > 8 ? 8 : N;
 };
 
+// the ring of the 8- / 12-wave workgroups (one per CU): KB-key blocks, as many stages as fit (capped at NST8)
+#ifndef PG_FA_KB8
+#define PG_FA_KB8 64
+#endif
+#ifndef PG_FA_NST8
+#define PG_FA_NST8 2
+#endif
+template <int DP, int DT>
+struct FaWide {
+  static constexpr int KB = PG_FA_KB8;
+  static constexpr int S = KB * DP * 2 + DT * 16 * KB * 2;
+  static constexpr int N = 163840 / S;
+  static constexpr int NST = N > PG_FA_NST8 ? PG_FA_NST8 : N;
+};
+
 template <int DP, int DT>
 static void launch_fa(int waves, int rpw, bool deep, dim3 grid, hipStream_t stream, const AttnArgs& a) {
   if (deep && waves == 4 && rpw == 1) {
@@ -1127,13 +1162,19 @@ static void launch_fa(int waves, int rpw, bool deep, dim3 grid, hipStream_t stre
     }
   }
   if constexpr (DP == 256) {
+    if (waves == 8 && rpw == 2) {
+      hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 2, 32, PG_FA_W8R2_NST>), grid, dim3(512), 0, stream, a);
+      return;
+    }
     if (waves == 12) {
-      hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 12, 1>), grid, dim3(768), 0, stream, a);
+      hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 12, 1, FaWide<DP, DT>::KB, FaWide<DP, DT>::NST>), grid, dim3(768), 0,
+                         stream, a);
       return;
     }
   }
   if (waves == 8)
-    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 1>), grid, dim3(512), 0, stream, a);
+    hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 8, 1, FaWide<DP, DT>::KB, FaWide<DP, DT>::NST>), grid, dim3(512), 0,
+                       stream, a);
   else if (waves == 2)
     hipLaunchKernelGGL((attn_fa_kernel<DP, DT, 2, 1>), grid, dim3(128), 0, stream, a);
   else if (waves == 1)
@@ -1204,7 +1245,16 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
     auto wgs = [&](int rows) { return (long)((Lq * G + rows - 1) / rows) * Hkv * B; };
     // two 16-row groups per wave (half the LDS fragment reads per flop) when the grid still fills the chip:
     // 8 waves x 32 rows for head_dim <= 96, else 4 waves x 32 rows (their accumulators need 1 wave / SIMD)
-    if (PG_FA_RPW == 2 && DP <= 96 && wgs(256) >= 256) {
+    auto rounds = [&](int rows) { return (wgs(rows) + 255) / 256; };
+    // head_dim 256, 8 waves x 32 rows on 32-key blocks (twice the flops per LDS fragment read of 16-row waves, two
+    // waves per SIMD at 256 registers): one round costs ~1.55 of an 8 x 16-row round (pt-896 x32 Gemma 5.03 vs
+    // 6.29 ms), so it is taken where its rounds cost less than those of the 8- and 12-wave forms (pt-448 x16 keeps
+    // 12 waves: 3 rounds of 256 rows cost more than 3 of 192)
+    if (PG_FA_W8R2 && DP == 256 && wgs(256) >= 256 &&
+        rounds(256) * 25 < rounds(128) * 16 && (!PG_FA_W12 || rounds(256) * 25 < rounds(192) * 24)) {
+      fa_waves = 8;
+      fa_rpw = 2;
+    } else if (PG_FA_RPW == 2 && DP <= 96 && wgs(256) >= 256) {
       fa_waves = 8;
       fa_rpw = 2;
     } else if (PG_FA_RPW == 2 && wgs(128) >= 256) {

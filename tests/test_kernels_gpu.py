@@ -295,7 +295,8 @@ def test_attention_vision_layout(B, N, nh, hd):
                                                   (8, 300, 8, 1, 256, False), (16, 130, 8, 1, 256, True),
                                                   (14, 300, 8, 1, 256, False),    # 12-wave flash kernel
                                                   (1, 1032, 8, 1, 256, False), (16, 1032, 8, 1, 256, False),  # pt-448
-                                                  (2, 4104, 8, 1, 256, False)])                              # pt-896
+                                                  (2, 4104, 8, 1, 256, False),                               # pt-896
+                                                  (32, 1000, 8, 1, 256, False)])      # 8 waves x 32 rows, 32-key blocks
 def test_attention_cache_layout_prefill_and_decode(B, L, nh, nkv, hd, masked):
     """Gemma: MQA/GQA from the static cache (K rows, V^T), prefill and split-KV decode, up to the pt-896 prefix
     (4104 keys: the multi-block, multi-round decode splits of BASELINE configs[4] over 4.2 k keys)."""
