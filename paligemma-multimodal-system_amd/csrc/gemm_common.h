@@ -31,6 +31,9 @@
 #ifndef PG_G256_STAGGER
 #define PG_G256_STAGGER 1       // gemm256: wave groups one barrier apart (MFMA of one || LDS reads of the other); +4-14%
 #endif
+#ifndef PG_G256_F8_BUF
+#define PG_G256_F8_BUF 1        // gemm256 fp8: operand pieces through buffer resources (two lane offsets, no spills)
+#endif
 #ifndef PG_G256_PREFETCH
 #define PG_G256_PREFETCH 1      // gemm256: LDS reads one phase ahead of the MFMAs
 #endif

@@ -331,9 +331,42 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   const int kt0 = z * ktiles_per_split;
   const int nk = max(0, min(K / 64 - kt0, ktiles_per_split));
 
+  // fp8 (PG_G256_F8_BUF): the pieces are loaded through buffer resources (buffer_load ... lds): a lane's two pieces
+  // of a half are 64 image rows apart (same swizzle), so every piece of a lane is ONE per-operand lane offset plus a
+  // uniform row / k offset, and rows past M / N read zeros (out of range of the resource) instead of being clamped.
+  // Two lane offsets live across the k loop instead of eight: the eight pushed the instance past 256 registers, and
+  // the spill reloads inside the loop waited vmcnt(0), draining the half-tiles in flight every k-step (pt-896 x32
+  // shapes: down 4.67 -> 4.00 ms, o_proj 0.81 -> 0.73 ms, gate/up 11.8 -> 9.9 ms; profiles/r06_g256_f8_buf_ab.txt).
+  constexpr bool BUF = F8 && !FRAG && PG_G256_F8_BUF;
+  unsigned la = 0, lw = 0;                         // (byte offsets < 4 GiB: host-checked, off32)
+  if constexpr (BUF) {
+    const int r0 = wave * 8 + (lane >> 3);           // piece rows r0 (it 0) and r0 + 64 (it 1)
+    const int c = (lane & 7) ^ ((r0 >> 1) & 7);
+    la = ((unsigned)r0 * (unsigned)lda + (unsigned)c * 8u) * 2u;
+    lw = ((unsigned)((r0 >> 5) * 64 + (r0 & 31)) * (unsigned)ldw + (unsigned)c * 8u) * 2u;
+  }
   auto stage = [&](int h, int kt) {
     char* dst = smem + ((kt & 1) * 4 + h) * HALF;
     const int k0 = (kt0 + kt) * 64;
+    if constexpr (BUF) {
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int blk = wave + 8 * it;
+        // uniform byte offset of this piece's rows at k0 (through readfirstlane: an SGPR computed here, so the sum
+        // below is not re-associated into per-piece loop-invariant lane offsets)
+        const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)(
+            h < 2 ? ((unsigned)(m0 + it * 128 + h * 64) * (unsigned)lda + (unsigned)k0) * 2u
+                  : ((unsigned)(n0 + it * 128 + (h - 2) * 32) * (unsigned)ldw + (unsigned)k0) * 2u));
+        // (the resource's size is the operand's M / N rows: pieces past them read zeros)
+        const auto rs = h < 2 ? __builtin_amdgcn_make_buffer_rsrc((void*)A, 0,
+                                                                  (int)((unsigned)e.M * (unsigned)lda * 2u), 0x00020000)
+                              : __builtin_amdgcn_make_buffer_rsrc((void*)W, 0,
+                                                                  (int)((unsigned)e.N * (unsigned)ldw * 2u), 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst + blk * 1024), 16,
+                                                 (int)((h < 2 ? la : lw) + so), 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int blk = wave * 2 + it;                 // 16 pieces of 8 rows x 128 B
@@ -601,8 +634,9 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(const float* __restr
 // ms per prefill), 2 every epilogue (gate/up 182 -> 211 ms and q|k|v 21 -> 48 ms: those instances still spill).
 // Round 6: with the down projection on MX rows (the 128 x 128 tile, 5.3 ms vs 6.3 on the 256 kernel), the o_proj
 // alone is faster on the 128 x 128 tile too: pt-896 x32 prefill 698.9 / 699.7 -> 695.3 / 696.5 ms
-// (profiles/r06_fp8_prefill_ab.jsonl), so 0
-#define PG_F8_G256 0
+// (profiles/r06_fp8_prefill_ab.jsonl), so 0 -- until the spill-free staging (PG_G256_F8_BUF): o_proj 765 -> 742 us
+// on the 256 kernel, q|k|v (RoPE epilogue, still spilling) 1.22 -> 2.29 ms, so 1 again
+#define PG_F8_G256 1
 #endif
 #ifndef PG_G256_MIN_TILES
 #define PG_G256_MIN_TILES 256   // large-M GEMM when its 256x256 grid fills every CU

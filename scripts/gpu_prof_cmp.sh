@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/$1; VAR=$2; VALS=$3; shift 3
 mkdir -p $O
 for v in $VALS; do
-  D=$O/${VAR}_$v
+  D=$O/${VAR}_$(basename $v)
   export $VAR=$v
   timeout -k 10 600 rocprofv3 --kernel-trace -d $D -o run --output-format csv -- python3 scripts/tune/prefill_big.py \
     --reps 2 "$@" > $D.log 2>&1 || { tail -5 $D.log; exit 1; }
