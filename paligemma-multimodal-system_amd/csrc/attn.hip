@@ -34,6 +34,18 @@
 #ifndef PG_FA_W8R2_HOIST
 #define PG_FA_W8R2_HOIST 4
 #endif
+#ifndef PG_FA_UNROLL
+#define PG_FA_UNROLL 1
+#endif
+#ifndef PG_FA_MASK_BRANCH
+#define PG_FA_MASK_BRANCH 1
+#endif
+#ifndef PG_FA_STAGE32
+#define PG_FA_STAGE32 1
+#endif
+#ifndef PG_FA_LAZY
+#define PG_FA_LAZY 8
+#endif
 #ifndef PG_FA_PRIO
 #define PG_FA_PRIO 0
 #endif
@@ -796,6 +808,9 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
   constexpr int STAGE = KIMG + VIMG;
   constexpr int KINS = KIMG / 1024, VINS = VIMG / 1024;   // glds wave-instructions per block
   constexpr int FA_HOIST = (DP == 256 && WAVES == 8 && RPW == 2) ? PG_FA_W8R2_HOIST : 0;
+  // lazy rescale for head_dim >= 128 only: at head_dim 72 (DT 5) the rescale is cheap and the branch cost more
+  // (pt-896 x32 SigLIP 3.79 -> 3.89 ms; Gemma 4.96 -> 4.75 ms)
+  constexpr int LAZY = DP >= 128 ? PG_FA_LAZY : 0;
   static_assert(KIMG % 1024 == 0 && VIMG % 1024 == 0 && NST * STAGE <= 163840, "stage images");
   __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
@@ -840,13 +855,19 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       const int ch = 4 * cq + (lane >> 4), key = 32 * (kg >> 1) + 8 * (i16 >> 2) + 4 * (kg & 1) + (i16 & 3);
       // chunks past D (D < DP) re-read chunk 0: the matching q dims are zero, and 0 * (finite K) = 0, whereas
       // the bytes past a head's D may be another tensor's never-written memory (NaN * 0 = NaN)
-      const bf16_t* src = kbase + (long)min(kb + key, Lkv - 1) * a.k_rs + (ch * 8 < D ? ch * 8 : 0);
+      const int kr = min(kb + key, Lkv - 1), kc = ch * 8 < D ? ch * 8 : 0;
+      // (PG_FA_STAGE32: uniform base + 32-bit lane offset -- the saddr form, no 64-bit address arithmetic per piece;
+      // the host takes this kernel only where a head's K rows and V^T rows span < 4 GiB)
+      const bf16_t* src = PG_FA_STAGE32 ? (const bf16_t*)((const char*)kbase + ((unsigned)kr * (unsigned)a.k_rs + (unsigned)kc) * 2u)
+                                        : kbase + (long)kr * a.k_rs + kc;
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(kimg + i * 1024), 16, 0, 0);
     }
     for (int i = wave; i < VINS; i += WAVES) {
       const int row = KB == 64 ? 8 * i + (lane >> 3) : 16 * i + (lane >> 2);
       const int cl = KB == 64 ? (lane & 7) ^ ((row >> 1) & 7) : (lane & 3) ^ ((row >> 2) & 2);
-      const bf16_t* src = vbase + (long)min(row, D - 1) * a.vt_ds + min(kb + 8 * cl, vkey_max);
+      const int vr = min(row, D - 1), vc = min(kb + 8 * cl, vkey_max);
+      const bf16_t* src = PG_FA_STAGE32 ? (const bf16_t*)((const char*)vbase + ((unsigned)vr * (unsigned)a.vt_ds + (unsigned)vc) * 2u)
+                                        : vbase + (long)vr * a.vt_ds + vc;
       __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(vimg + i * 1024), 16, 0, 0);
     }
   };
@@ -873,6 +894,9 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
     if (sb < nblk) stage(kb0 + sb * KB, sb);
   // static priority for the second-dispatched half of a 2-wave-per-SIMD workgroup (tuning knob)
   if constexpr (PG_FA_PRIO) if (WAVES >= 8 && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#if PG_FA_UNROLL == 2
+#pragma unroll 2
+#endif
   for (int ib = 0; ib < nblk; ++ib) {
     const int kb = kb0 + ib * KB;
     // block ib has landed once at most (blocks issued after it) * P of this wave's pieces are outstanding
@@ -911,6 +935,9 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[4 * kt + j] = sc[i][kt][j];
       if (kb + KB > Lkv) {
+        // (the empty volatile asm keeps this a branch: if-converted, the ~50 compares and selects of the key mask ran
+        // on every block, a third of the softmax's VALU)
+        if constexpr (PG_FA_MASK_BRANCH) asm volatile("");
 #pragma unroll
         for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
@@ -922,8 +949,25 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       for (int j = 1; j < 4 * NKT; ++j) bm = fmaxf(bm, x[j]);
       bm = max_xor16(bm);
       bm = max_xor32(bm);
-      const float mn = fmaxf(m[i], bm * a.scale_log2);   // = the max of the scaled scores (scaling is monotonic)
-      const float alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+      float mn = fmaxf(m[i], bm * a.scale_log2);         // = the max of the scaled scores (scaling is monotonic)
+      float alpha;
+      if constexpr (LAZY > 0) {
+        // lazy rescale: the running max moves (and O, l are rescaled) only when some row of the wave gained more than
+        // 2^PG_FA_LAZY; otherwise the exponents are taken against the stale max (P <= 2^PG_FA_LAZY: same bf16
+        // relative precision, fp32 O and l).  The volatile asm keeps it a branch (if-converted, the rescale of O ran
+        // on every block)
+        alpha = 1.0f;
+        if (__builtin_amdgcn_ballot_w64(mn > m[i] + (float)LAZY)) {
+          asm volatile("");
+          alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+#pragma unroll
+          for (int tt = 0; tt < DT; ++tt) o[i][tt] *= alpha;
+          m[i] = mn;
+        }
+        mn = m[i];
+      } else {
+        alpha = __builtin_amdgcn_exp2f(m[i] - mn);
+      }
       const f32x2 s2 = {a.scale_log2, a.scale_log2}, n2 = {-mn, -mn};
       f32x2 rs2 = {0.f, 0.f};
 #pragma unroll
@@ -937,10 +981,12 @@ __global__ __launch_bounds__(WAVES * 64) void attn_fa_kernel(AttnArgs a) {
       rs = sum_xor16(rs);
       rs = sum_xor32(rs);
       l[i] = l[i] * alpha + rs;
-      m[i] = mn;
-      if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O
+      if constexpr (LAZY == 0) {
+        m[i] = mn;
+        if (__builtin_amdgcn_ballot_w64(alpha != 1.0f)) {   // a row's max moved: rescale O
 #pragma unroll
-        for (int tt = 0; tt < DT; ++tt) o[i][tt] *= alpha;
+          for (int tt = 0; tt < DT; ++tt) o[i][tt] *= alpha;
+        }
       }
       // P^T operand of the 32-key steps; slot 8g+j <-> key 32h + 8g + j
 #pragma unroll
@@ -1241,7 +1287,10 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
   // LDS-DMA flash kernel for every unmasked prefill; 8 waves (128 rows) per workgroup once that fills the chip
   int fa_waves = 0, fa_rpw = 1;
   bool fa_deep = false;
-  if (split_keys == 0 && mask == nullptr && aligned && lkv_dev == nullptr && PG_ATTN_FA) {
+  // (the flash kernel stages by 32-bit offsets from a head's K / V^T base)
+  const bool off32 = (unsigned long)(Lkv + 64) * (unsigned long)k_rs * 2ul < (1ul << 32) &&
+                     (unsigned long)D * (unsigned long)vt_ds * 2ul < (1ul << 32);
+  if (split_keys == 0 && mask == nullptr && aligned && off32 && lkv_dev == nullptr && PG_ATTN_FA) {
     auto wgs = [&](int rows) { return (long)((Lq * G + rows - 1) / rows) * Hkv * B; };
     // two 16-row groups per wave (half the LDS fragment reads per flop) when the grid still fills the chip:
     // 8 waves x 32 rows for head_dim <= 96, else 4 waves x 32 rows (their accumulators need 1 wave / SIMD)
