@@ -392,7 +392,7 @@ def make_topp(inference):
     print("topp: kept sizes", [len(cases[f"c{i}_kept_ids"]) for i in range(4)])
 
 
-def make_main(mp, inference):
+def make_main(mp, inference, full=False):
     """BASELINE configs[0] end to end: the reference's own inference.main (inference.py:109-150: load_hf_model ->
     PaliGemmaProcessor -> test_inference, CPU, greedy) on the model directory and RGBA image of tests/main_fixture.py.
     Stores what it prints (the prompt + decoded line), the generated ids (captured at the tokenizer's decode) and each
@@ -402,8 +402,11 @@ def make_main(mp, inference):
     from transformers import PreTrainedTokenizerBase
     d = tempfile.mkdtemp()
     try:
-        cfg = MF.write_model_dir(os.path.join(d, "model"))
-        img = MF.write_image(os.path.join(d, "pic.png"))
+        cfg = MF.write_model_dir(os.path.join(d, "model"), full=full)
+        img = MF.write_image(os.path.join(d, "pic.png"), MF.FULL_IMAGE_SEED if full else MF.IMAGE_SEED)
+        ntok = MF.FULL_MAX_TOKENS if full else MF.MAX_TOKENS
+        if full:
+            torch.set_num_threads(os.cpu_count())
         decoded_ids, margins = [], []
         real_decode = PreTrainedTokenizerBase.decode
 
@@ -424,7 +427,7 @@ def make_main(mp, inference):
         try:
             with contextlib.redirect_stdout(buf):
                 inference.main(model_path=os.path.join(d, "model"), prompt=MF.PROMPT, image_file_path=img,
-                               max_tokens_to_generate=MF.MAX_TOKENS, do_sample=False, only_cpu=True)
+                               max_tokens_to_generate=ntok, do_sample=False, only_cpu=True)
         finally:
             PreTrainedTokenizerBase.decode, mp.PaliGemmaForConditionalGeneration.forward = real_decode, real_fwd
     finally:
@@ -434,7 +437,7 @@ def make_main(mp, inference):
     out = {"stdout": np.array(buf.getvalue()), "printed": np.array(printed),
            "ids": np.array(decoded_ids[-1], dtype=np.int64), "margins": np.array(margins, dtype=np.float32),
            "vocab_size": np.int64(cfg["text_config"]["vocab_size"]), "image_token_index": np.int64(cfg["image_token_index"])}
-    np.savez_compressed(os.path.join(HERE, "main.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "main_full.npz" if full else "main.npz"), **out)
     print("main:", repr(printed), "| ids", out["ids"].tolist(), "| min margin", float(out["margins"].min()))
 
 
@@ -454,6 +457,8 @@ if __name__ == "__main__":
         make_large(mp, inference, proc, "pt448", configs.PT_448, [1234, 1235], steps=8, row_stride=16)
     if "processor" in which:
         make_processor(proc)
+    if "mainfull" in which:       # BASELINE configs[0] at PaliGemma-3B-224 size through the reference's inference.main
+        make_main(mp, inference, full=True)
     if "pt224wc" in which:        # free-running greedy parity (better-conditioned recipe)
         make_pt224wc(mp, inference, proc)
     if "pt896" in which:          # BASELINE configs[4]

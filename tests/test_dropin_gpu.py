@@ -213,6 +213,39 @@ def test_module_loop_grows_cache_past_initial_capacity(model, golden, W):
     assert torch.equal(k_all[:, :, :L], fresh.k_cache[0][:, :, :L])
 
 
+def test_inference_main_full_size_matches_reference(golden, tmp_path, capsys):
+    """BASELINE configs[0] at its own size: a PaliGemma-3B-224-dimensioned model directory (config.json with the
+    HF pt-224 dimensions, a 5.8 GB bf16 model.safetensors of the better-conditioned synthetic recipe generated on the
+    device, the offline tokenizer) and an RGBA PNG -> the drop-in's inference.main (load_hf_model -> processor ->
+    test_inference -> decode / print; /root/reference/utils.py:9-38, inference.py:109-150).  The reference's own
+    inference.main ran on the same files in the development container (tests/golden/make_golden.py mainfull ->
+    tests/golden/main_full.npz, min top1-top2 margin 0.12 over its 8 greedy steps): the 8 free-running ids and the
+    printed line must be identical.  (Ids past the offline tokenizer's few words decode to nothing in both stacks.)"""
+    import main_fixture as MF
+    from transformers import PreTrainedTokenizerBase
+    import inference
+    g = golden("main_full")
+    cfg = MF.write_model_dir(str(tmp_path / "model"), full=True, gpu=True)
+    assert cfg["text_config"]["vocab_size"] == int(g["vocab_size"]) == 257216
+    assert cfg["image_token_index"] == int(g["image_token_index"])
+    img = MF.write_image(str(tmp_path / "pic.png"), MF.FULL_IMAGE_SEED)
+    seen = []
+    real = PreTrainedTokenizerBase.decode
+
+    def decode(self, token_ids, *a, **k):
+        seen.append([int(t) for t in token_ids])
+        return real(self, token_ids, *a, **k)
+    PreTrainedTokenizerBase.decode = decode
+    try:
+        inference.main(model_path=str(tmp_path / "model"), prompt=MF.PROMPT, image_file_path=img,
+                       max_tokens_to_generate=MF.FULL_MAX_TOKENS, do_sample=False)
+    finally:
+        PreTrainedTokenizerBase.decode = real
+    out = capsys.readouterr().out
+    assert seen and seen[-1] == g["ids"].tolist(), (seen[-1], g["ids"].tolist())
+    assert str(g["printed"]) in out, (out[-500:], str(g["printed"]))
+
+
 def test_inference_main_end_to_end_matches_reference(golden, tmp_path, capsys):
     """BASELINE configs[0] ("single-image greedy decode via inference.py") end to end through the drop-in: a model
     directory (config.json + reference-keyed model.safetensors + tokenizer files) and an RGBA PNG shaped like the
