@@ -195,6 +195,14 @@ int pg_attention(const void* q, long q_rs, void* o, long o_rs, const void* k, lo
 int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                     void* o, long o_rs, hipStream_t stream);
 
+/* The attention weights the reference's modules return, out fp32 [B][Hq][Lq][Lkv] with pg_attention's q / k / mask
+ * addressing: probs = 1 softmax(q . k^T * scale + mask) (gemma.py:358), probs = 0 the scaled scores + mask before the
+ * softmax (siglip.py:157 returns those).  The module API's opt-in (the flash kernels never form this matrix; at
+ * pt-896 x32 it is 34 GB per layer). */
+int pg_attn_probs(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const float* mask,
+                  long mask_bs, long mask_rs, int B, int Lq, int Lkv, int Hq, int Hkv, int D, float scale,
+                  int probs, float* out, hipStream_t stream);
+
 /* Batched split-KV decode attention with the split merge in the same launch (gemma.py:307-339 for one new position
  * per row; replaces pg_attention(split) + pg_attn_combine for B > 2, ABI 5).  The kcap/32 cache blocks of a
  * (batch, kv head) are cut into nsplit contiguous ranges for splits of nw (2 or 4) waves, nb rounds each (nw*nsplit <=

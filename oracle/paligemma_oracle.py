@@ -205,8 +205,9 @@ def siglip_embeddings(W: dict, vcfg: dict, pixel_values: np.ndarray) -> np.ndarr
     return (emb + W[pre + "positional_embeddings.weight"][None, : nh * nw]).astype(F32)
 
 
-def siglip_attention(W: dict, lp: str, vcfg: dict, x: np.ndarray) -> np.ndarray:
-    """SiglipAttention.forward (modeling_siglip.py:65-157)."""
+def siglip_attention(W: dict, lp: str, vcfg: dict, x: np.ndarray, weights_out: Optional[list] = None) -> np.ndarray:
+    """SiglipAttention.forward (modeling_siglip.py:65-157); weights_out receives the attention weights it returns
+    (:157: the scaled scores from before the softmax)."""
     B, N, E = x.shape
     nh = vcfg["num_attention_heads"]
     hd = E // nh
@@ -218,6 +219,8 @@ def siglip_attention(W: dict, lp: str, vcfg: dict, x: np.ndarray) -> np.ndarray:
     q = q16(q).reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
     v = q16(v).reshape(B, N, nh, hd).transpose(0, 2, 1, 3)
     s = (q @ k.transpose(0, 1, 3, 2)) * scale                          # :96-100
+    if weights_out is not None:
+        weights_out.append(s)                                           # :157 returns the pre-softmax scores
     p = softmax_lastdim(s)                                              # :122
     o = q16(p) @ v                                                      # :136
     o = o.transpose(0, 2, 1, 3).reshape(B, N, E)                        # :148-153
@@ -309,8 +312,10 @@ def rms_norm(x: np.ndarray, w: np.ndarray, eps: float = 1e-6) -> np.ndarray:
 
 
 def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
-                    position_ids: np.ndarray, mask: np.ndarray, kv_cache: Optional[KVCache]):
-    """GemmaAttention.forward (modeling_gemma.py:264-358)."""
+                    position_ids: np.ndarray, mask: np.ndarray, kv_cache: Optional[KVCache],
+                    weights_out: Optional[list] = None):
+    """GemmaAttention.forward (modeling_gemma.py:264-358); weights_out receives the attention weights it returns
+    (:358)."""
     B, L, _ = x.shape
     nh, nkv = tcfg["num_attention_heads"], tcfg["num_key_value_heads"]
     hd = tcfg.get("head_dim", 256)
@@ -333,6 +338,8 @@ def gemma_attention(W: dict, lp: str, tcfg: dict, layer_idx: int, x: np.ndarray,
     assert mask is not None, "Attention Mask needss to be provided"    # :325
     s = s + mask                                                        # :326
     p = softmax_lastdim(s)                                              # :329
+    if weights_out is not None:
+        weights_out.append(p)
     o = q16(p) @ v                                                      # :339
     if o.shape != (B, nh, L, hd):                                       # :341-345
         raise ValueError("Size Mismatch")

@@ -1417,6 +1417,72 @@ extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, cons
   return 0;
 }
 
+// The attention weights the reference's modules return, for callers of the module API that read them: probs = 1
+// (modeling_gemma.py:358) the softmax(Q K^T * scale + mask) probabilities, probs = 0 (modeling_siglip.py:157, which
+// returns its scores from before the softmax) the scaled scores (+ mask), fp32.  Not on the hot path -- the flash
+// kernels never form this matrix.  One 256-thread workgroup per (b, q head, query row): the q row in LDS as fp32,
+// each thread a key at a time (fp32 dot product of the bf16 q / k rows), then the row max, exp and sum as
+// workgroup reductions; out[((b * Hq + hq) * Lq + pos) * Lkv + key].
+__global__ __launch_bounds__(256) void attn_probs_kernel(const bf16_t* __restrict__ q, long q_rs,
+                                                         const bf16_t* __restrict__ k, long k_bs, long k_hs, long k_rs,
+                                                         const float* __restrict__ mask, long mask_bs, long mask_rs,
+                                                         int Lq, int Lkv, int Hq, int Hkv, int D, float scale,
+                                                         int probs, float* __restrict__ out) {
+  __shared__ float qs[256];
+  __shared__ float red[8];
+  const int pos = blockIdx.x, hq = blockIdx.y, b = blockIdx.z, t = threadIdx.x;
+  const int kvh = hq / (Hq / Hkv);
+  const bf16_t* qr = q + ((long)b * Lq + pos) * q_rs + (long)hq * D;
+  for (int d = t; d < D; d += 256) qs[d] = bf2f(qr[d]);
+  __syncthreads();
+  const bf16_t* kb = k + (long)b * k_bs + (long)kvh * k_hs;
+  const float* mr = mask ? mask + (long)b * mask_bs + (long)pos * mask_rs : nullptr;
+  float* orow = out + (((long)b * Hq + hq) * Lq + pos) * Lkv;
+  auto block_reduce = [&](float v, bool is_max) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float w = __shfl_xor(v, o, 64);
+      v = is_max ? fmaxf(v, w) : v + w;
+    }
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int i = 1; i < 4; ++i) r = is_max ? fmaxf(r, red[i]) : r + red[i];
+    __syncthreads();
+    return r;
+  };
+  float mx = -INFINITY;
+  for (int j = t; j < Lkv; j += 256) {
+    const bf16_t* kr = kb + (long)j * k_rs;
+    float acc = 0.f;
+    for (int d = 0; d < D; ++d) acc += qs[d] * bf2f(kr[d]);
+    const float sc = acc * scale + (mr ? mr[j] : 0.f);
+    orow[j] = sc;
+    mx = fmaxf(mx, sc);
+  }
+  if (!probs) return;
+  mx = block_reduce(mx, true);
+  float sum = 0.f;
+  for (int j = t; j < Lkv; j += 256) {
+    const float e = __expf(orow[j] - mx);
+    orow[j] = e;
+    sum += e;
+  }
+  const float inv = 1.0f / block_reduce(sum, false);
+  for (int j = t; j < Lkv; j += 256) orow[j] *= inv;
+}
+
+extern "C" int pg_attn_probs(const void* q, long q_rs, const void* k, long k_bs, long k_hs, long k_rs, const float* mask,
+                             long mask_bs, long mask_rs, int B, int Lq, int Lkv, int Hq, int Hkv, int D, float scale,
+                             int probs, float* out, hipStream_t stream) {
+  PG_REQUIRE(q && k && out && B > 0 && Lq > 0 && Lkv > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && D > 0 && D <= 256);
+  PG_REQUIRE(Lq <= 65535 * 32 && Hq <= 65535 && B <= 65535);
+  hipLaunchKernelGGL(attn_probs_kernel, dim3(Lq, Hq, B), dim3(256), 0, stream, (const bf16_t*)q, q_rs,
+                     (const bf16_t*)k, k_bs, k_hs, k_rs, mask, mask_bs, mask_rs, Lq, Lkv, Hq, Hkv, D, scale, probs, out);
+  PG_LAUNCH_CHECK();
+  return 0;
+}
+
 #if PG_ATTN_STAMPS
 // diagnostic variant only (not in the product library): copy the decode-split stamps to the host
 extern "C" int pg_attn_stamps_read(void* host, int n) {

@@ -8,8 +8,9 @@ kernel layouts (bf16, fused q|k|v, interleaved gate/up) and caches the pack unti
 parameters change.  Every forward requires CUDA(HIP) tensors: there is no CPU path.
 
 Deliberate, output-invariant differences:
-  * ``GemmaAttention.forward`` returns ``(attn_output, None)``: the softmax weights are
-    never materialised (flash attention); no reference caller uses them (:398-403).
+  * ``GemmaAttention.forward`` returns ``(attn_output, None)`` unless ``module.return_attn_weights``
+    (or PG_ATTN_WEIGHTS=1) asks for the softmax weights (:358; pg_attn_probs forms them): the flash
+    kernels never materialise them, and no reference caller uses them (:398-403).
   * ``KVCache`` keeps the reference API (``update`` / ``num_items`` / ``k_cache`` /
     ``v_cache``) on top of a static, in-place HBM buffer (no torch.cat per step, :54-55).
   * batch > 1 decode works (the reference builds (1, B) position ids and fails, :189-191).
@@ -303,6 +304,7 @@ class GemmaAttention(nn.Module):
         self.q_proj = nn.Linear(self.hidden_size, self.num_heads * self.head_dim, bias=config.attention_bias)
         self.o_proj = nn.Linear(self.hidden_size, self.hidden_size, bias=config.attention_bias)
         self._pk = _PackCache()
+        self.return_attn_weights = ops.ATTN_WEIGHTS
 
     def packed(self):
         def build():
@@ -358,7 +360,12 @@ class GemmaAttention(nn.Module):
                       scale=1.0 / math.sqrt(hd), mask=mask, mask_bs=L * Lkv, mask_rs=Lkv)
         out = torch.empty(B * L, self.hidden_size, dtype=torch.float32, device=dev)
         ops.gemm(o, wo, out, epi=ops.EPI_F32, bias=bo)
-        return out.view(B, L, self.hidden_size), None
+        weights = None
+        if self.return_attn_weights:        # the softmax matrix the reference returns (:358), formed on request only
+            weights = ops.attn_probs(q, nh * hd, st.k[self.layer_idx], st.Smax * kvd, hd, kvd, B=B, Lq=L, Lkv=Lkv,
+                                     Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd), mask=mask, mask_bs=L * Lkv,
+                                     mask_rs=Lkv)
+        return out.view(B, L, self.hidden_size), weights
 
 
 class DecoderLayer(nn.Module):

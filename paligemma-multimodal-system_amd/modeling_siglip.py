@@ -6,7 +6,9 @@ kernel sequence (im2col -> patch GEMM with bias+position epilogue -> per layer L
 fused QKV GEMM (V written transposed), flash attention, out GEMM, LayerNorm, fc1 GEMM+GELU,
 fc2 GEMM -> post-LayerNorm); the sub-modules' forwards run their own part through the same
 kernels.  The residual stream is fp32, MFMA operands bf16.  HIP tensors only.
-``SiglipAttention.forward`` returns ``(out, None)``: the softmax matrix is never materialised.
+``SiglipAttention.forward`` returns ``(out, weights)``: the flash kernel never forms the score matrix, so weights is
+None unless asked for (``module.return_attn_weights = True`` or PG_ATTN_WEIGHTS=1); then pg_attn_probs forms what
+the reference returns there (:157), the scaled scores from before the softmax.
 """
 from __future__ import annotations
 
@@ -91,6 +93,7 @@ class SiglipAttention(nn.Module):
         self.query_proj = nn.Linear(self.embed_dim, self.embed_dim)
         self.out_proj = nn.Linear(self.embed_dim, self.embed_dim)
         self._pk = _Pack()
+        self.return_attn_weights = ops.ATTN_WEIGHTS
 
     def packed(self):
         ps = [self.query_proj.weight, self.key_proj.weight, self.value_proj.weight, self.out_proj.weight,
@@ -117,7 +120,11 @@ class SiglipAttention(nn.Module):
                       B=B, Lq=N, Lkv=N, Hq=self.num_heads, Hkv=self.num_heads, D=hd, scale=self.scale)
         out = torch.empty(M, E, dtype=torch.float32, device=x.device)
         ops.gemm(o, wo, out, epi=ops.EPI_F32, bias=bo)
-        return out.view(B, N, E), None
+        weights = None
+        if self.return_attn_weights:        # what the reference returns (:157): its scaled scores from before the softmax
+            weights = ops.attn_probs(qkv, 3 * E, qkv[:, E:], N * 3 * E, hd, 3 * E, B=B, Lq=N, Lkv=N,
+                                     Hq=self.num_heads, Hkv=self.num_heads, D=hd, scale=self.scale, probs=False)
+        return out.view(B, N, E), weights
 
 
 class SiglipMLP(nn.Module):

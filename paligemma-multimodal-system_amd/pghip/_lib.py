@@ -43,6 +43,7 @@ SIGNATURES = {
     "pg_attention": [vp, i64, vp, i64, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
                      i32, i32, i32, vp, i32, i32, i32, f32, i32, i32, vp, vp, i32, vp, vp, vp],
     "pg_attn_combine": [vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
+    "pg_attn_probs": [vp, i64, vp, i64, i64, i64, vp, i64, i64, i32, i32, i32, i32, i32, i32, f32, i32, vp, vp],
     "pg_attn_decode": [vp, i64, vp, i64, vp, vp, i32, i32, vp, i32, i32, i32, f32, i32, i32, i32, i32, vp, vp, vp,
                        vp, vp, i64, vp],
     "pg_rope_kv_write": [vp, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, i32, i32, vp, vp],

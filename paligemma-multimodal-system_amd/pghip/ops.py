@@ -315,6 +315,25 @@ def attn_combine(part_o, part_ml, o, o_rs, *, B, Hq, Hkv, D, nsplit):
     _lib.call("pg_attn_combine", _p(part_o), _p(part_ml), B, Hq, Hkv, D, nsplit, _p(o), o_rs, _s())
 
 
+# the module API's attention weights (modeling_*.py: SiglipAttention / GemmaAttention return them when asked): off by
+# default -- the flash kernels never form the softmax matrix, which at pt-896 x32 is 34 GB per layer
+ATTN_WEIGHTS = os.environ.get("PG_ATTN_WEIGHTS", "0") == "1"
+
+
+def attn_probs(q, q_rs, k, k_bs, k_hs, k_rs, *, B, Lq, Lkv, Hq, Hkv, D, scale, mask=None, mask_bs=0, mask_rs=0,
+               probs=True, out=None) -> torch.Tensor:
+    """The attention weights [B][Hq][Lq][Lkv] fp32 with pg_attention's addressing (pg_attn_probs): the softmax
+    probabilities (probs, GemmaAttention's second output) or the scaled scores before the softmax (SiglipAttention's),
+    on request only."""
+    if out is None:
+        out = torch.empty(B, Hq, Lq, Lkv, dtype=torch.float32, device=q.device)
+    if mask is not None:
+        _chk(mask, torch.float32, "mask")
+    _lib.call("pg_attn_probs", _p(q), q_rs, _p(k), k_bs, k_hs, k_rs, _p(mask), mask_bs, mask_rs, B, Lq, Lkv, Hq, Hkv,
+              D, float(scale), int(bool(probs)), _p(out), _s())
+    return out
+
+
 DECODE_MAX_SPLITS = int(os.environ.get("PG_DECODE_MAX_SPLITS", "8"))
 
 

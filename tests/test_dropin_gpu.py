@@ -103,6 +103,53 @@ def test_submodules_vs_oracle(model, W):
         assert err(dl.input_layernorm(h.cuda()), O.rms_norm(h.numpy(), W[tp + "input_layernorm.weight"])) < 1e-5
 
 
+def test_attention_weights_as_the_reference_returns_them(model, W):
+    """With module.return_attn_weights the attention modules return what the reference returns as their second
+    output (pg_attn_probs): SiglipAttention the scaled scores from before the softmax (modeling_siglip.py:96-100,157),
+    GemmaAttention the masked softmax probabilities (modeling_gemma.py:314-329,358), over the cached keys in the
+    decode step too; default None (the flash kernels never form the matrix)."""
+    from modeling_gemma import KVCache
+    vc, tc = ocfg.TINY["vision_config"], ocfg.TINY["text_config"]
+    torch.manual_seed(3)
+    x = torch.randn(2, 16, vc["hidden_size"])
+    lp = "vision_tower.model.encoder.layers.1.self_attn."
+    att = model.vision_tower.model.encoder.layers[1].self_attn
+    ga = model.language_model.model.layers[0].self_attn
+    try:
+        att.return_attn_weights = ga.return_attn_weights = True
+        with torch.no_grad():
+            _, w = att(x.cuda())
+        ref = []
+        O.siglip_attention(W, lp, vc, x.numpy(), weights_out=ref)
+        assert w.shape == ref[0].shape and w.dtype == torch.float32
+        assert err(w, ref[0]) < 1e-2                       # bf16 q / k operands, fp32 scores
+        B, L, H = 2, 6, tc["hidden_size"]
+        h = torch.randn(B, L, H) * 0.5
+        pos = torch.arange(L)[None].expand(B, L)
+        mask = torch.triu(torch.full((L, L), -1e9), 1)[None, None].expand(B, 1, L, L)
+        tp = "language_model.model.layers.0.self_attn."
+        kv, okv = KVCache(), O.KVCache()
+        with torch.no_grad():
+            _, gw = ga(hidden_states=h.cuda(), position_ids=pos.cuda(), kv_cache=kv, attention_mask=mask.cuda())
+        gref = []
+        O.gemma_attention(W, tp, tc, 0, h.numpy(), pos.numpy(), mask.numpy(), okv, weights_out=gref)
+        assert gw.shape == gref[0].shape == (B, tc["num_attention_heads"], L, L)
+        assert np.abs(gw.cpu().numpy() - gref[0]).max() < 1e-2
+        assert torch.allclose(gw.sum(-1).cpu(), torch.ones(B, tc["num_attention_heads"], L), atol=1e-5)
+        h2 = torch.randn(B, 1, H) * 0.5
+        p2, m2 = torch.full((B, 1), L), torch.zeros(B, 1, 1, L + 1)
+        with torch.no_grad():
+            _, gw2 = ga(hidden_states=h2.cuda(), position_ids=p2.cuda(), kv_cache=kv, attention_mask=m2.cuda())
+        gref2 = []
+        O.gemma_attention(W, tp, tc, 0, h2.numpy(), p2.numpy(), m2.numpy(), okv, weights_out=gref2)
+        assert gw2.shape == (B, tc["num_attention_heads"], 1, L + 1)
+        assert np.abs(gw2.cpu().numpy() - gref2[0]).max() < 1e-2
+    finally:
+        att.return_attn_weights = ga.return_attn_weights = False
+    with torch.no_grad():
+        assert att(x.cuda())[1] is None
+
+
 def test_gemma_causal_lm_with_causal_mask_and_cache(model, W):
     """GemmaForCausalLM used on its own with a causal additive mask, then one cached decode step."""
     from modeling_gemma import KVCache
