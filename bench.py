@@ -8,8 +8,10 @@ token count is fixed).  value = generated tokens / step wall t
 Multi-GPU (torch.distributed.run, one rank per GPU): --parallel dp (default) runs one request per
 rank (independent replicas, weak scaling; no data-path collective); value = all ranks' tokens /
 max-over-ranks time.  --parallel tp shards the Gemma decoder over all ranks (q heads, gate/up
-columns, vocabulary; RCCL SUM all-reduce after o_proj and down_proj) and runs ONE
-request across them (strong scaling: per-token latency); value = that request's tokens / time.
+columns, vocabulary; a SUM all-reduce after o_proj and down_proj over xGMI peer stores: one-shot for
+decode-size slabs, reduce-scatter + all-gather for prefill chunks; --comm rccl uses the process
+group's collective instead) and runs ONE request across them (strong scaling: per-token latency); value = that
+request's tokens / time.  `--gpus N` without WORLD_SIZE launches the N ranks itself (a torch.distributed.run child).
 
 Extra fields: prefill_ms, decode_tok_s, decode HBM fraction; "roofline" for the dominant
 kernel (the decode gate/up GEMV, HIP events on the stream it runs on); "cpu_baseline" = the
@@ -220,7 +222,8 @@ class Runner:
 def tp_leg(spec, rank, world, dist, steps=2):
     """One tensor-parallel run over the ranks [0, spec["tp"]) (q heads, gate/up columns and the
     vocabulary split; SigLIP data-parallel over the images when the batch covers the ranks; decode-size
-    collectives as pg_allreduce_xgmi / pg_allgather_xgmi one-shot peer stores over xGMI, larger ones on RCCL),
+    collectives as pg_allreduce_xgmi / pg_allgather_xgmi one-shot peer stores over xGMI, prefill chunks on the
+    reduce-scatter + all-gather pg_allreduce_xgmi_rs, anything beyond their buffers on the process group),
     timing `steps` requests of spec's workload.  Every rank of the world takes part in the phase agreements;
     ranks outside the TP group idle.  Phases: communicator setup, engine build (local only: packing, no
     collective), a first request (prefill + decode-graph capture), timed requests.  After each phase all ranks
@@ -383,8 +386,8 @@ def main():
     ap.add_argument("--gen-tokens", type=int, default=128)
     ap.add_argument("--parallel", default="dp", choices=["dp", "tp"])
     ap.add_argument("--comm", default="xgmi", choices=["xgmi", "rccl"],
-                    help="TP all-reduce: pg_allreduce_xgmi for decode-size slabs (RCCL/gloo beyond its buffer), "
-                    "or the process group's collective only")
+                    help="TP all-reduce: the xGMI peer-store kernels (one-shot for decode-size slabs, reduce-scatter + "
+                    "all-gather for prefill chunks; RCCL/gloo beyond their buffers), or the process group's collective only")
     ap.add_argument("--fp8", action="store_true",
                     help="Gemma linears as fp8 e4m3 (per-channel / per-row scales) for GEMMs over 16 rows, as BASELINE "
                     "configs[4]")
