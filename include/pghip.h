@@ -21,7 +21,8 @@
 extern "C" {
 #endif
 
-int pg_abi_version(void);   /* 12: PgFusedArgs.status (FX_ADD range check), amax_zero on the bf16 GEMV, the xGMI
+int pg_abi_version(void);   /* 13: PG_EPI_F32_RES (the prefill residual add in the producing tile GEMM), pg_attn_probs
+                              (the modules' attention weights); 12: PgFusedArgs.status (FX_ADD range check), amax_zero on the bf16 GEMV, the xGMI
                               reduce-scatter + all-gather (pg_allreduce_xgmi_rs) and err diagnostics; 11: PgFusedArgs mx_out / mx_in (MX block-scaled fp8 decode MLP rows); 10: PG_EPI_FX_ADD + PgFusedArgs.fx (bit-reproducible decode residual); 9: PgFusedArgs amax_out / amax_in (pro_mode 5) / amax_zero, PG_ATTN_PIPE; 8: pg_allreduce_xgmi_slabs, PG_EPI_F32_ADD; 7: pg_attn_decode's optional fp8 row copy (q8 / q8_scale / q8_ld); 6: decode-order KV copies (PgFusedArgs.kd / vd; pg_attention, pg_attn_decode read
                               them); 5: pg_attn_decode; 4: the measured-slower decode variants removed */
 /* sha256 (hex, 64 chars + NUL) of the csrc/ sources, include/pghip.h and the compile flags this library was built
@@ -43,13 +44,16 @@ enum {
   PG_EPI_F32_FIN = 7,       /* M <= 4: F32 slabs, then the last split of each 16-column tile adds them into
                                fin_resid and writes ss_out (the residual add of gemma.py:401,416 + the next
                                RMSNorm's sum of squares); pg_gemm_fused only                                  */
-  PG_EPI_F32_ADD = 8        /* (ABI 8) M <= 16, pro_mode 0 or 2: C f32 [M][ldc] += acc (+ bias by split 0) by
+  PG_EPI_F32_ADD = 8,       /* (ABI 8) M <= 16, pro_mode 0 or 2: C f32 [M][ldc] += acc (+ bias by split 0) by
                                hardware float atomic adds in any split order (the residual add of gemma.py:401,416
                                with no slab or ticket; the next GEMV normalises with pro_mode 1, nsplit 0)       */
-  PG_EPI_FX_ADD = 9         /* (ABI 10) M <= 16, bf16, pro_mode 0 or 2: C int64 [M][ldc] += round(acc * 2^32) (+ bias by
+  PG_EPI_FX_ADD = 9,        /* (ABI 10) M <= 16, bf16, pro_mode 0 or 2: C int64 [M][ldc] += round(acc * 2^32) (+ bias by
                                split 0) by 64-bit integer atomics -- F32_ADD's residual add, but the fixed-point sum is
                                exact and so the same bits in any split order (bit-reproducible decode).  C is the
                                PgFusedArgs.fx accumulator that pro_mode 1 and PG_EPI_F32_FIN consumers read      */
+  PG_EPI_F32_RES = 10       /* (ABI 13) tile GEMMs (M > 16), ksplit 1, pro_mode 0: C f32 [M][ldc] += acc + bias -- the
+                               prefill residual add (siglip:203-221, gemma.py:401,416) done by the producing GEMM, one
+                               workgroup per output, so the next norm reads the residual alone (nsplit 0)        */
 };
 
 /* Fused-operation arguments of pg_gemm_fused (M <= 16 for the prologues). */

@@ -18,7 +18,7 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   if (frag && !fp8) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
                        (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||
                         epi == PG_EPI_QKV_ROPE || epi == PG_EPI_F32_FIN || epi == PG_EPI_F32_ADD ||
-                        epi == PG_EPI_FX_ADD));
+                        epi == PG_EPI_FX_ADD || epi == PG_EPI_F32_RES));
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{bias, C, ldc, M, N, aux, aux_rows, (bf16_t*)aux_out, aux_ld, aux_n, f};
@@ -54,13 +54,16 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
                                         ldc == N);
   if (epi == PG_EPI_F32_ADD) PG_REQUIRE((M <= 16 || (fp8 && frag && M <= 32)) && (f.pro_mode == 0 || f.pro_mode == 2) &&
                                         ldc >= N);
+  // (ABI 13) the residual add moved into the producing tile GEMM: one producer per output, C 16-B aligned rows
+  if (epi == PG_EPI_F32_RES) PG_REQUIRE(M > 16 && ksplit == 1 && f.pro_mode == 0 && ldc >= N && ldc % 4 == 0 &&
+                                        ((uintptr_t)C & 15) == 0 && !f.mx_out);
   if (epi == PG_EPI_FX_ADD) PG_REQUIRE(M <= 16 && !fp8 && (f.pro_mode == 0 || f.pro_mode == 2) && ldc >= N &&
                                        ((uintptr_t)C & 15) == 0 && ldc % 2 == 0);
   if (f.mx_in && frag) PG_REQUIRE(fp8 && epi != PG_EPI_F32_ADD && M <= 32 && f.pro_mode == 0 && K % 128 == 0 &&
                                    A != nullptr && ((uintptr_t)f.mx_in & 15) == 0 &&
                                    (!f.ss_in || (f.ss_n > 0 && f.ss_n <= 4 && f.ss_ld >= f.ss_n && K == 1024 * f.ss_n)));
   // (ABI 12) the prefill tile form: MX rows [M][K] with scales [M][K/32] into the 256 x 256 fp32-slab GEMM
-  if (f.mx_in && !frag) PG_REQUIRE(fp8 && epi == PG_EPI_F32 && M > 32 && f.pro_mode == 0 && K % 128 == 0 &&
+  if (f.mx_in && !frag) PG_REQUIRE(fp8 && (epi == PG_EPI_F32 || epi == PG_EPI_F32_RES) && M > 32 && f.pro_mode == 0 && K % 128 == 0 &&
                                    A != nullptr && ((uintptr_t)f.mx_in & 3) == 0 && !f.ss_in &&
                                    (size_t)M * (size_t)(K / 32) < (1ull << 32) &&
                                    (size_t)M * (size_t)lda < (1ull << 32) && (size_t)N * (size_t)ldw < (1ull << 32));

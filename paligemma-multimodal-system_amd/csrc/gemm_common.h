@@ -55,6 +55,8 @@ enum {
   PG_EPI_FX_ADD = 9,        // GEMV (M <= 16, bf16): C int64 [M][ldc] += rn(acc * 2^32) (+ bias by split 0) with
                             // 64-bit integer atomics: F32_ADD's one-round-trip tail, but the sum is exact and so
                             // independent of the split order -- bit-reproducible decode (PgFusedArgs.fx)
+  PG_EPI_F32_RES = 10,      // tile GEMMs (M > 16), ksplit 1: C f32 [M][ldc] += acc + bias -- the residual add of the
+                            // next norm done by the producer (each output has ONE producing workgroup: plain RMW)
 };
 
 // the fixed-point residual accumulator (PG_EPI_FX_ADD, PgFusedArgs.fx): value = q * 2^-32, |value| < 2^31
@@ -338,6 +340,14 @@ __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) if (n0 + j < e.N) C[n0 + j] = v[j];
+    }
+  } else if constexpr (EPI == PG_EPI_F32_RES) {
+    float* C = (float*)e.C + (size_t)m * e.ldc;
+    if (n0 + 3 < e.N) {
+      *(f32x4*)(C + n0) = *(const f32x4*)(C + n0) + v;      // (resid + (acc + bias): the norm kernel's one add)
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) if (n0 + j < e.N) C[n0 + j] = C[n0 + j] + v[j];
     }
   } else if constexpr (EPI == PG_EPI_F32_POS) {
     float* C = (float*)e.C + (size_t)m * e.ldc;

@@ -712,7 +712,7 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
       return;
     }
   }
-  if constexpr (F8 && (EPI == PG_EPI_F32 || EPI == PG_EPI_BF16_GELU_MUL)) {
+  if constexpr (F8 && (EPI == PG_EPI_F32 || EPI == PG_EPI_F32_RES || EPI == PG_EPI_BF16_GELU_MUL)) {
     if (e.f.mx_in || e.f.mx_out) {
       // (ABI 12) MX rows in (the prefill down projection) / MX h out (the prefill gate/up): the 128 x 128 fp8 tile, whose
       // waves own 32 rows x 64 W rows -- one 32-column h block per row (out), two row subtiles of scales (in)
@@ -732,7 +732,7 @@ static void launch_tile(const bf16_t* A, int lda, const bf16_t* W, int ldw, int 
   const int t256 = ((e.M + 255) / 256) * ((e.N + 255) / 256);
   // (fp8 on the 256 x 256 kernel addresses its operands by 32-bit byte offsets: both must be < 4 GiB)
   const bool off32 = (size_t)e.M * lda * 2 < (1ull << 32) && (size_t)e.N * ldw * 2 < (1ull << 32);
-  constexpr bool g256 = !F8 || PG_F8_G256 == 2 || (PG_F8_G256 == 1 && EPI == PG_EPI_F32);
+  constexpr bool g256 = !F8 || PG_F8_G256 == 2 || (PG_F8_G256 == 1 && (EPI == PG_EPI_F32 || EPI == PG_EPI_F32_RES));
   if (g256 && (!F8 || off32) && t256 * ksplit >= PG_G256_MIN_TILES && (ksplit == 1 || EPI == PG_EPI_F32)) {
     const int kts = (K / 64 + ksplit - 1) / ksplit;
     hipLaunchKernelGGL((gemm256_kernel<EPI, FRAG, F8>), dim3(t256, 1, ksplit), dim3(512), 0, st, A, lda, W, ldw, K, kts,
@@ -770,6 +770,9 @@ int pg_dispatch_tile(int epi, bool frag, bool f8, const bf16_t* A, int lda, cons
         launch_tile<PG_EPI_BF16_GELU_MUL, false, true>(A, lda, W, ldw, K, ksplit, e, st, false, n64);
         return 0;
       case PG_EPI_F32: launch_tile<PG_EPI_F32, false, true>(A, lda, W, ldw, K, ksplit, e, st, false, n64); return 0;
+      case PG_EPI_F32_RES:
+        launch_tile<PG_EPI_F32_RES, false, true>(A, lda, W, ldw, K, ksplit, e, st, false, n64);
+        return 0;
       case PG_EPI_QKV_ROPE:
         launch_tile<PG_EPI_QKV_ROPE, false, true>(A, lda, W, ldw, K, ksplit, e, st, false, n64);
         return 0;
@@ -787,6 +790,7 @@ int pg_dispatch_tile(int epi, bool frag, bool f8, const bf16_t* A, int lda, cons
     PG_CASE(PG_EPI_BF16)
     PG_CASE(PG_EPI_BF16_GELU_MUL)
     PG_CASE(PG_EPI_F32)
+    PG_CASE(PG_EPI_F32_RES)
     PG_CASE(PG_EPI_QKV_ROPE)
     PG_CASE_ROWMAJOR(PG_EPI_BF16_GELU)
     PG_CASE_ROWMAJOR(PG_EPI_F32_POS)

@@ -583,7 +583,7 @@ extern "C" int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, f
 // ABI 4: the measured-slower decode variants removed (pg_attn_oproj, pg_decode_attn_block, pg_decode_mlp_block,
 // pg_decode_mlp_engine, pg_gateup_bank, pg_prefetch, the *_stamps diagnostics) and PgFusedArgs slimmed to the
 // fields the default path uses; pg_source_hash added.
-extern "C" int pg_abi_version(void) { return 12; }
+extern "C" int pg_abi_version(void) { return 13; }
 
 // sha256 (hex) over the csrc/ sources, include/pghip.h and the compile flags this library was built from
 // (pghip/build.py passes it as PG_SOURCE_HASH): the loader compares it with the tree it runs from, so a stale

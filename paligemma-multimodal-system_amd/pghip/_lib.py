@@ -82,7 +82,7 @@ class PgHipError(RuntimeError):
     pass
 
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 def source_hash(lib=None) -> str:

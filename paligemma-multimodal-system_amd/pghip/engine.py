@@ -147,6 +147,13 @@ class PaliGemmaEngine:
     # columns (each wave owns one block per row) and the 256 x 256 fp8 down GEMM stages the block scales beside h --
     # the row quantiser launch between them (and half of h's bytes) is gone
     MX_PREFILL = os.environ.get("PG_MX_PREFILL", "1") != "0"
+    # prefill linears that end a residual branch (SigLIP o / fc2, Gemma o / down) with ONE split on one rank add into
+    # the residual in their epilogue (PG_EPI_F32_RES, ABI 13): the next norm reads the residual alone, 4 B per element
+    # less than a slab write + slab read + residual rewrite; bit-identical (the same one fp32 add)
+    PREFILL_RES = os.environ.get("PG_PREFILL_RES", "1") != "0"
+    # ... from this many rows on: pt-896 x32 prefill 672-675 -> 665-667 ms; at pt-448 x16 (16 k rows) level to 0.5%
+    # slower (85.4-85.6 vs 84.9-85.1 ms; profiles/r06_prefill_res_ab.jsonl), so off there
+    PREFILL_RES_MIN_M = int(os.environ.get("PG_PREFILL_RES_MIN_M", "65536"))
 
     AMAX_LD = 32                     # one 128-B line per row maximum (the gate/up atomics of 32 rows spread out)
     # 128-k chunks of h per down workgroup (8 or 16): bf16 h costs twice fp8's bytes per workgroup, so the split
@@ -272,20 +279,29 @@ class PaliGemmaEngine:
         s_2 = ops.gemm_ksplit(Bs * N, hv, w.v_inter)
         ks_v = self._key_split_args("v", Bs, N, N, nh, nh, hd)
         part = self._buf("v_part", (max(s_o, s_2), M, hv), torch.float32)
+        res = self.PREFILL_RES and M >= max(17, self.PREFILL_RES_MIN_M)
+        res_o, res_2 = res and s_o == 1, res and s_2 == 1
         ns = 0
         for L in w.vl:
             ops.norm_residual(resid, L["ln1_w"], b=L["ln1_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
-                              nsplit=ns, out=xn)
+                              nsplit=ns, out=xn, write_resid=ns > 0)
             ops.gemm(xn, L["qkv_w"], qkv, epi=ops.EPI_BF16_VT, bias=L["qkv_b"], aux_out=vt, aux_ld=M + 32,
                      aux_n=2 * hv, split_m=Bs * N)
             ops.attention(qkv, 3 * hv, attn, hv, qkv[:, hv:], N * 3 * hv, hd, 3 * hv, vt, N, hd * (M + 32), M + 32,
                           B=B, Lq=N, Lkv=N, Hq=nh, Hkv=nh, D=hd, scale=1.0 / (hd ** 0.5), **ks_v)
-            self._gemm_cols(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
+            if res_o:
+                self._gemm_cols(attn, L["o_w"], resid, epi=ops.EPI_F32_RES, bias=L["o_b"])
+            else:
+                self._gemm_cols(attn, L["o_w"], part, epi=ops.EPI_F32, bias=L["o_b"], ksplit=s_o)
             ops.norm_residual(resid, L["ln2_w"], b=L["ln2_b"], mode=ops.NORM_LAYER, eps=w.v_eps, partials=part,
-                              nsplit=s_o, out=xn)
+                              nsplit=0 if res_o else s_o, out=xn, write_resid=not res_o)
             self._gemm_cols(xn, L["fc1_w"], h, epi=ops.EPI_BF16_GELU, bias=L["fc1_b"], split_m=Bs * N)
-            self._gemm_cols(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
-            ns = s_2
+            if res_2:
+                self._gemm_cols(h, L["fc2_w"], resid, epi=ops.EPI_F32_RES, bias=L["fc2_b"])
+                ns = 0
+            else:
+                self._gemm_cols(h, L["fc2_w"], part, epi=ops.EPI_F32, bias=L["fc2_b"], ksplit=s_2)
+                ns = s_2
             if taps is not None:                                          # debug: residual after the layer
                 taps.append((resid + part[:ns].sum(0)).clone())
         hid = torch.empty(M, hv, dtype=torch.float32, device=self.device) if want_hidden else None
@@ -343,7 +359,7 @@ class PaliGemmaEngine:
                           B=B, Lq=L, Lkv=L, Hq=nh, Hkv=nkv, D=hd, scale=1.0 / math.sqrt(hd),
                           mask=mask, mask_bs=(mask.stride(0) if mask is not None else 0),
                           mask_rs=(mask.stride(-2) if mask is not None else 0), **ks_t)
-            n_o = self._row_parallel(attn, Lw, "o", part, T, s_o)
+            n_o = self._row_parallel(attn, Lw, "o", part, T, s_o, resid=x_resid)
             xin = self._norm(x_resid, Lw["post_w"], part, n_o, xn, T)
             if self._mx_prefill(T):
                 # MX h: e4m3 rows + block scales from the gate/up epilogue, straight into the down GEMM
@@ -351,10 +367,10 @@ class PaliGemmaEngine:
                 hs = self._buf("t_hs", (T, I // 32), torch.uint8)
                 x8, xs = xin
                 ops.gemm8(x8, xs, Lw["gu_w8"], Lw["gu_s8"], h8, epi=ops.EPI_BF16_GELU_MUL, M=T, mx_out=hs)
-                ns = self._row_parallel(("mx", h8, hs), Lw, "down", part, T, s_d)
+                ns = self._row_parallel(("mx", h8, hs), Lw, "down", part, T, s_d, resid=x_resid)
             else:
                 self._lin(xin, Lw, "gu", h, ops.EPI_BF16_GELU_MUL, T)
-                ns = self._row_parallel(h, Lw, "down", part, T, s_d)
+                ns = self._row_parallel(h, Lw, "down", part, T, s_d, resid=x_resid)
             if taps is not None:
                 taps.append((x_resid + part[:ns].sum(0)).clone())
         cache.length = L
@@ -523,8 +539,10 @@ class PaliGemmaEngine:
             H = resid.shape[-1]
             x8 = self._buf(f"x8_{H}", (M, H), torch.uint8)
             xs = self._buf(f"xs_{H}", (M,), torch.float32)
-            return ops.norm_residual_fp8(resid, norm_w, x8, xs, mode=ops.NORM_RMS, partials=part, nsplit=nsplit)
-        ops.norm_residual(resid, norm_w, mode=ops.NORM_RMS, partials=part, nsplit=nsplit, out=xn)
+            return ops.norm_residual_fp8(resid, norm_w, x8, xs, mode=ops.NORM_RMS, partials=part, nsplit=nsplit,
+                                         write_resid=nsplit > 0)
+        ops.norm_residual(resid, norm_w, mode=ops.NORM_RMS, partials=part, nsplit=nsplit, out=xn,
+                          write_resid=nsplit > 0)
         return xn
 
     def _allreduce_slabs(self, part: torch.Tensor, ns: int) -> int:
@@ -536,13 +554,22 @@ class PaliGemmaEngine:
             return ns
         return self.comm.all_reduce_slabs(part[:ns], ns)
 
-    def _row_parallel(self, x: torch.Tensor, Lw: dict, name: str, part: torch.Tensor, T: int, ks: int) -> int:
+    def _row_parallel(self, x: torch.Tensor, Lw: dict, name: str, part: torch.Tensor, T: int, ks: int,
+                      resid: Optional[torch.Tensor] = None) -> int:
         """A row-parallel prefill linear (o_proj / down_proj) into fp32 partial slabs; returns how many slabs the
         next norm must add.  One rank: `ks` split-K slabs.  Tensor parallel: ONE slab, completed by a SUM all-reduce
         -- a rank's split-K slabs are summed locally first (slab_sum), so every sub-block moves T*H*4 bytes instead
         of ks times that.  From 2 * AR_CHUNK_ROWS rows on, the rows run as chunks with one split each: chunk c's
         all-reduce is issued asynchronously (comm stream) and overlaps chunk c+1's GEMM."""
         if self.tp == 1:
+            # (not where the bf16 GEMM runs as row blocks: its ragged tail takes a deeper split of its own, which a
+            # one-split epilogue cannot -- pt-448 x16 prefill 82.9 -> 86.6 ms with it)
+            row_blocks = (not self._fp8_rows(T) and self.ROW_BLOCKS and
+                          self._row_head(T, self.w.hidden, 1) > 0)
+            if (resid is not None and self.PREFILL_RES and ks == 1 and T >= max(17, self.PREFILL_RES_MIN_M)
+                    and not row_blocks):
+                self._lin(x, Lw, name, resid, ops.EPI_F32_RES, T)     # the residual add in the epilogue
+                return 0
             self._lin(x, Lw, name, part, ops.EPI_F32, T, ksplit=ks)
             return ks
         # at most AR_CHUNK_ROWS rows per chunk (4096 x 2048 fp32 = the xGMI exchange's 2^23 cap: no chunk spills to

@@ -15,7 +15,7 @@ import torch
 from . import _lib
 
 EPI_BF16, EPI_BF16_GELU, EPI_BF16_GELU_MUL, EPI_F32, EPI_F32_POS, EPI_BF16_VT, EPI_QKV_ROPE, EPI_F32_FIN, \
-    EPI_F32_ADD, EPI_FX_ADD = range(10)
+    EPI_F32_ADD, EPI_FX_ADD, EPI_F32_RES = range(11)
 FX_SCALE = 2.0 ** 32   # PG_EPI_FX_ADD: the int64 accumulator holds round(value * 2^32)
 PRO_NONE, PRO_RMSNORM, PRO_ATTN_COMBINE, PRO_RMSNORM_FIN, PRO_X_RSTD = range(5)
 NORM_LAYER, NORM_RMS = 0, 1
@@ -65,11 +65,13 @@ def gemm(A: torch.Tensor, W: torch.Tensor, out: torch.Tensor, *, epi: int = EPI_
     if bias is not None:
         _chk(bias, torch.float32, "bias")
     ldc = out.stride(-2) if out.dim() >= 2 else out.shape[-1]
-    if epi == EPI_F32:
+    if epi in (EPI_F32, EPI_F32_RES):
         _chk(out, torch.float32, "out")
         need = (ksplit * M - 1) * ldc + N                                # last element touched, in elements
         if out.storage_offset() + need > out.untyped_storage().nbytes() // out.element_size():
             raise ValueError("pghip.gemm: partial output too small")
+        if epi == EPI_F32_RES and (ksplit != 1 or M <= 16):
+            raise ValueError("pghip.gemm: EPI_F32_RES (out += acc + bias) is a one-split tile epilogue (M > 16)")
     elif epi == EPI_F32_POS:
         _chk(out, torch.float32, "out")
     else:

@@ -55,7 +55,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.pg_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.pg_abi_version() == _lib.ABI_VERSION == 13
 
 
 def test_library_matches_source_tree():
@@ -355,3 +355,22 @@ def test_library_has_no_mfma_result_read_hazards():
         total += n
         assert bad == [], bad[:5]
     assert total > 10000, total                      # the GEMM / GEMV / attention kernels were all scanned
+
+
+def test_c_abi_header_compiles_as_c_and_cpp():
+    """include/pghip.h is the drop-in boundary a C / C++ binding includes: it must compile on its own as both (round 6
+    found a missing enum comma that only a compiler would catch)."""
+    import shutil
+    import subprocess
+    import tempfile
+    inc = os.path.join(ROOT, "include")
+    src = '#include "pghip.h"\nint main(void) { return (int)PG_EPI_F32_RES + (int)sizeof(PgFusedArgs) * 0; }\n'
+    with tempfile.TemporaryDirectory() as d:
+        for cc, ext in (("gcc", "c"), ("g++", "cpp")):
+            if shutil.which(cc) is None:
+                pytest.skip(f"{cc} not installed")
+            f = os.path.join(d, "t." + ext)
+            open(f, "w").write(src)
+            r = subprocess.run([cc, "-fsyntax-only", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I", inc, "-I",
+                                "/opt/rocm/include", f], capture_output=True, text=True)
+            assert r.returncode == 0, (cc, r.stderr[-2000:])

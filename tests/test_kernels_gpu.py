@@ -840,6 +840,45 @@ def test_quant_fp8_rows_bit_identical_to_host_rule(M, K):
     assert err(_deq(q, s), x.float()) < 0.07          # e4m3: 3 mantissa bits
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 384, 512), (4200, 4096, 640), (33, 1152, 1152)])
+def test_gemm_f32_res_adds_into_the_residual_bit_exactly(M, N, K):
+    """PG_EPI_F32_RES (ABI 13): the producing tile GEMM adds acc + bias into the fp32 residual in its epilogue; equal
+    bit for bit to the PG_EPI_F32 slab plus the one fp32 add the norm kernel makes (resid + slab), on the bf16 tile
+    and 256 x 256 kernels (row-major and fragment-packed W), the fp8 kernels (row scales) and the fp8 MX-rows-in
+    tile; the columns past N and the rows of another GEMM untouched."""
+    from pghip import ops
+    from pghip.weights import frag_pack, quant_rows_fp8
+    A, W = rnd(M, K, seed=61), rnd(N, K, scale=1 / math.sqrt(K), seed=62)
+    bias = torch.randn(N).cuda()
+    resid0 = torch.randn(M, N + 8, device="cuda")                 # ldc > N: the pad columns must stay
+    cases = [("bf16", lambda out, e: ops.gemm(A, W, out, epi=e, bias=bias))]
+    if K % 64 == 0 and N % 16 == 0:
+        Wf = frag_pack(W)
+        cases.append(("bf16 frag", lambda out, e: ops.gemm(A, Wf, out, epi=e | ops.W_FRAG, bias=bias)))
+    if K % 128 == 0 and M > 16:
+        a8, sa = ops.quant_fp8(A)
+        w8, sw = quant_rows_fp8(W)
+        cases.append(("fp8", lambda out, e: ops.gemm8(a8, sa, w8, sw, out, epi=e, bias=bias)))
+    for name, run in cases:
+        slab = torch.empty(M, N + 8, device="cuda")
+        run(slab, ops.EPI_F32)
+        out = resid0.clone()
+        run(out, ops.EPI_F32_RES)
+        assert torch.equal(out[:, :N], resid0[:, :N] + slab[:, :N]), name
+        assert torch.equal(out[:, N:], resid0[:, N:]), name
+    if M > 32 and K % 128 == 0:                                  # MX rows in (the prefill down projection's form)
+        q = torch.randint(0, 126, (M, K), dtype=torch.uint8, device="cuda")     # finite e4m3 bytes
+        sc = torch.randint(120, 134, (M, K // 32), dtype=torch.uint8, device="cuda")
+        w8, sw = quant_rows_fp8(W)
+        slab = torch.empty(M, N + 8, device="cuda")
+        ops.gemm8(q, None, w8, sw, slab, epi=ops.EPI_F32, mx_in=sc)
+        out = resid0.clone()
+        ops.gemm8(q, None, w8, sw, out, epi=ops.EPI_F32_RES, mx_in=sc)
+        assert torch.equal(out[:, :N], resid0[:, :N] + slab[:, :N])
+    with pytest.raises(ValueError):                                # one split only
+        ops.gemm(A, W, resid0.clone(), epi=ops.EPI_F32_RES, ksplit=2)
+
+
 @pytest.mark.parametrize("M,N,K", [(300, 384, 512), (1024, 2048, 2048), (4096, 4096, 256), (4200, 4096, 640)])
 def test_gemm_fp8_matches_fp32_matmul_of_dequantised_operands(M, N, K):
     """PG_FP8 GEMM (16x16x128 block-scaled MFMA, unit block scales, row scales in the epilogue) on the tile
