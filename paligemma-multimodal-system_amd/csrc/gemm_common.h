@@ -327,6 +327,30 @@ __device__ __forceinline__ void epi_qkv_rope4(const EpiArgs& e, int m, int n0, f
   epi_qkv_rope4_pr(e, m, n0, v, pr);
 }
 
+// PG_EPI_F32_RES in two halves, so a row subtile's residual loads are all issued before its first store (the
+// compiler cannot move a load of C above an earlier store to C: one load latency per store otherwise)
+__device__ __forceinline__ f32x4 res_load4(const EpiArgs& e, int m, int n0) {
+  f32x4 r = {0.f, 0.f, 0.f, 0.f};
+  if (m >= e.M || n0 >= e.N) return r;
+  const float* C = (const float*)e.C + (size_t)m * e.ldc;
+  if (n0 + 3 < e.N) return *(const f32x4*)(C + n0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) if (n0 + j < e.N) r[j] = C[n0 + j];
+  return r;
+}
+__device__ __forceinline__ void res_store4(const EpiArgs& e, int m, int n0, f32x4 v, f32x4 r) {
+  if (m >= e.M || n0 >= e.N) return;
+  if (e.bias) v += load4_guard(e.bias, n0, e.N);
+  float* C = (float*)e.C + (size_t)m * e.ldc;
+  const f32x4 o = r + v;                                 // (resid + (acc + bias): the norm kernel's one add)
+  if (n0 + 3 < e.N) {
+    *(f32x4*)(C + n0) = o;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) if (n0 + j < e.N) C[n0 + j] = o[j];
+  }
+}
+
 // Store 4 consecutive columns n0..n0+3 of row m (values v).  z = split index.
 template <int EPI>
 __device__ __forceinline__ void epi_store4(const EpiArgs& e, int m, int n0, f32x4 v, int z) {

@@ -240,6 +240,25 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tile_kernel(const bf16_t* __r
 
   // epilogue: acc[i][j] lane holds C[m = m0+wm*(BM/WM)+i*16+(lane&15)][n = n0+wn*(BN/WN)+j*16+4*(lane>>4) + 0..3]
   const int q = 4 * (lane >> 4);
+  if constexpr (EPI == PG_EPI_F32_RES) {
+    // all NI x NJ residual loads of the wave in flight before its stores
+    f32x4 rr[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15), n = n0 + wn * (BN / WN) + j * 16 + q;
+        if constexpr (F8) scale_acc(e, m, n, acc[i][j]);
+        rr[i][j] = res_load4(e, m, n);
+      }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        res_store4(e, m0 + wm * (BM / WM) + i * 16 + (lane & 15), n0 + wn * (BN / WN) + j * 16 + q, acc[i][j],
+                   rr[i][j]);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
@@ -555,6 +574,31 @@ __global__ __launch_bounds__(512) void gemm256_kernel(const bf16_t* __restrict__
   // epilogue: acc[i][j] lane holds C[m][n..n+3], m = m0 + wr*128 + (i/4)*64 + (i%4)*16 + (lane&15),
   // n = n0 + wc*64 + (j/2)*32 + (j%2)*16 + 4*(lane>>4)
   const int q = 4 * (lane >> 4);
+  if constexpr (EPI == PG_EPI_F32_RES) {
+    // two row subtiles (i, i + 1: rows m, m + 16) at a time: their 8 residual loads in flight before the stores
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const int m = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);
+      f32x4 rr[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + q;
+        if constexpr (F8) {
+          scale_acc(e, m, n, acc[i][j]);
+          scale_acc(e, m + 16, n, acc[i + 1][j]);
+        }
+        rr[0][j] = res_load4(e, m, n);
+        rr[1][j] = res_load4(e, m + 16, n);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wc * 64 + (j >> 1) * 32 + (j & 1) * 16 + q;
+        res_store4(e, m, n, acc[i][j], rr[0][j]);
+        res_store4(e, m + 16, n, acc[i + 1][j], rr[1][j]);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = m0 + wr * 128 + (i >> 2) * 64 + (i & 3) * 16 + (lane & 15);

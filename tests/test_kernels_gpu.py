@@ -823,10 +823,12 @@ def _deq(q, s):
     return q.view(torch.float8_e4m3fn).float() * s[:, None]
 
 
-@pytest.mark.parametrize("M,K", [(1, 8), (7, 2048), (300, 16384), (64, 1152), (32, 16384), (3, 24576), (2, 40960)])
+@pytest.mark.parametrize("M,K", [(1, 8), (7, 2048), (300, 16384), (64, 1152), (32, 16384), (3, 24576), (2, 40960),
+                                 (4103, 2048), (1030, 1152), (2049, 4096), (1024, 24)])   # the wave-per-row form
 def test_quant_fp8_rows_bit_identical_to_host_rule(M, K):
     """pg_quant_fp8 (row absmax / 448 scale, RNE e4m3) gives the same bytes and scales as the host rule the
-    weights use (weights.quant_rows_fp8), including an all-zero row (scale 1)."""
+    weights use (weights.quant_rows_fp8), including an all-zero row (scale 1); from 1024 rows (K <= 4096) the
+    one-wave-per-row kernel, a ragged last workgroup included."""
     from pghip import ops
     from pghip.weights import quant_rows_fp8
     x = rnd(M, K, scale=3.0, seed=51)
