@@ -8,8 +8,9 @@
  *
  * Conventions: plain device pointers + sizes; every call enqueues on `stream`
  * (hipStream_t; pass torch.cuda.current_stream().cuda_stream), never allocates,
- * never synchronises, and returns 0 or a hipError_t code (hipErrorInvalidValue for
- * a rejected shape).  bf16 = IEEE bfloat16 bits in uint16; "f32" = float.
+ * never synchronises, and returns 0 or a hipError_t code (hipErrorInvalidValue, before
+ * any HIP call, for a rejected shape or a null required operand).  bf16 = IEEE bfloat16
+ * bits in uint16; "f32" = float.
  * Buffers are owned by the caller (PyTorch's caching allocator).
  */
 #ifndef PGHIP_H

@@ -53,6 +53,7 @@
 
 #define PG_XG_MAXW 8
 #define PG_XG_MAXWG 64
+#define PG_XG_MAXCAP (1L << 40)             // floats per slot: keeps the buffer byte counts inside a long
 #define PG_XG_CHUNK 8192                    // floats per chunk (32 KB)
 #define PG_XG_FLAG_BYTES 4096
 #define PG_XG_TIMEOUT_TICKS 2000000000ull   // 20 s of the 100 MHz constant clock
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void allreduce_rs_kernel(const float* __restri
 }
 
 extern "C" int pg_xgmi_buffer_bytes(int world, long cap, long* bytes) {
-  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && cap > 0 && cap % 4 == 0 && bytes != nullptr);
+  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && cap > 0 && cap <= PG_XG_MAXCAP && cap % 4 == 0 && bytes != nullptr);
   *bytes = PG_XG_FLAG_BYTES + 2L * world * cap * (long)sizeof(float);
   return 0;
 }
@@ -236,7 +237,8 @@ extern "C" int pg_xgmi_buffer_bytes(int world, long cap, long* bytes) {
 static long rs_chunks(int world, long rs_cap) { return (rs_cap + (long)world * PG_XR_P - 1) / ((long)world * PG_XR_P); }
 
 extern "C" int pg_xgmi_rs_buffer_bytes(int world, long rs_cap, long* bytes) {
-  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && rs_cap > 0 && rs_cap % 4 == 0 && bytes != nullptr);
+  PG_REQUIRE(world >= 1 && world <= PG_XG_MAXW && rs_cap > 0 && rs_cap <= PG_XG_MAXCAP && rs_cap % 4 == 0 &&
+             bytes != nullptr);
   *bytes = PG_XR_FLAG_BYTES + 4L * rs_chunks(world, rs_cap) * world * PG_XR_P * (long)sizeof(float);
   return 0;
 }

@@ -1267,7 +1267,8 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
                             int D, float scale, int split_keys, int nsplit, float* part_o, float* part_ml,
                             int kcap, const void* kd, const void* vd, hipStream_t stream) {
   PG_REQUIRE(B > 0 && Lq > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && D > 0 && D % 8 == 0 && D <= 256);
-  PG_REQUIRE(kcap >= 0 && kcap % 32 == 0);
+  // (split mode writes partials only: o is read by nobody, the merge is pg_attn_combine's or the o_proj prologue's)
+  PG_REQUIRE(kcap >= 0 && kcap % 32 == 0 && q && (split_keys == 0 ? o != nullptr : (part_o && part_ml)));
   const int G = Hq / Hkv;
   const int DP = ((D + 31) / 32) * 32;
   const int DT = (D + 15) / 16;
@@ -1365,7 +1366,8 @@ extern "C" int pg_attention(const void* q, long q_rs, void* o, long o_rs, const 
 
 extern "C" int pg_attn_combine(const float* part_o, const float* part_ml, int B, int Hq, int Hkv, int D, int nsplit,
                                void* o, long o_rs, hipStream_t stream) {
-  PG_REQUIRE(Hq % Hkv == 0 && Hq / Hkv <= 16 && nsplit <= 256);
+  PG_REQUIRE(part_o && part_ml && o && B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && nsplit >= 1 &&
+             nsplit <= 256 && D > 0);
   const int DT = (D + 15) / 16;
   PG_REQUIRE(D <= 256 && D % 4 == 0 && o_rs % 4 == 0 && ((uintptr_t)o & 7) == 0 && nsplit <= 256);
   hipLaunchKernelGGL(attn_combine_kernel, dim3(B * Hq), dim3(256), 0, stream, part_o, part_ml, nsplit, Hq / Hkv,
@@ -1384,7 +1386,7 @@ extern "C" int pg_attn_decode(const void* q, long q_rs, void* o, long o_rs, cons
                               int Lkv, const int* lkv_dev, int Hq, int Hkv, int D, float scale, int kcap, int nsplit,
                               int nw, int nb, float* part_o, float* part_ml, int* counters, void* q8,
                               float* q8_scale, long q8_ld, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && (D == 32 || D == 256));
+  PG_REQUIRE(q && B > 0 && Hq > 0 && Hkv > 0 && Hq % Hkv == 0 && Hq / Hkv <= 16 && (D == 32 || D == 256));
   const bool pipe = (nw & PG_ATTN_PIPE) != 0 && nb >= 2;      // the double-buffered form (head_dim 256, 4 waves)
   nw &= ~PG_ATTN_PIPE;
   // the fp8 copy: the merging workgroup holds the whole row (one kv head, one item per thread)

@@ -10,10 +10,10 @@ static int gemm_impl(const void* A, int lda, const void* W, int ldw, const float
   const bool m1 = (epi_flags & PG_TILE_M1) != 0;
   const bool n64 = (epi_flags & PG_TILE_N64) != 0;
   const int epi = epi_flags & 0xFF;
-  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8 | PG_TILE_M1 | PG_TILE_N64)) == 0);
+  PG_REQUIRE((epi_flags & ~(0xFF | PG_W_FRAG | PG_FP8 | PG_TILE_M1 | PG_TILE_N64)) == 0 && epi <= PG_EPI_F32_RES);
   if (m1) PG_REQUIRE(!fp8 && !n64 && M >= 256 && M <= 288 && (fa == nullptr || fa->pro_mode == 0));
   if (n64) PG_REQUIRE(M > 16);
-  PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1);
+  PG_REQUIRE(M > 0 && N > 0 && K > 0 && ksplit >= 1 && W != nullptr && C != nullptr);
   PG_REQUIRE(K % 32 == 0 && ldw >= K && (N % 4) == 0);
   if (frag && !fp8) PG_REQUIRE(N % 16 == 0 && K % 64 == 0 && ldw == K &&
                        (epi == PG_EPI_BF16 || epi == PG_EPI_BF16_GELU_MUL || epi == PG_EPI_F32 ||

@@ -848,7 +848,7 @@ int pg_dispatch_tile(int epi, bool frag, bool f8, const bf16_t* A, int lda, cons
 // C = epilogue(sum_z part[z]) for a GEMM run as PG_EPI_F32 with ksplit slabs (bias was applied to slab 0)
 extern "C" int pg_gemm_finalize(const float* part, int nsplit, void* C, int ldc, int M, int N, int epi,
                                 void* aux_out, int aux_ld, int aux_n, const PgFusedArgs* fa, hipStream_t stream) {
-  PG_REQUIRE(part != nullptr && nsplit >= 1 && M > 0 && N > 0 && N % 4 == 0);
+  PG_REQUIRE(part != nullptr && C != nullptr && nsplit >= 1 && M > 0 && N > 0 && N % 4 == 0);
   PgFusedArgs f{};
   if (fa) f = *fa;
   EpiArgs e{nullptr, C, ldc, M, N, nullptr, 0, (bf16_t*)aux_out, aux_ld, aux_n, f};

@@ -35,7 +35,7 @@ __global__ void im2col_kernel(const float* __restrict__ px, int B, int C, int H,
 
 extern "C" int pg_patch_im2col(const float* px, int B, int C, int H, int W, int p, void* out, int ldk,
                                hipStream_t stream) {
-  PG_REQUIRE(ldk >= C * p * p && H >= p && W >= p);
+  PG_REQUIRE(px && out && B > 0 && C > 0 && p > 0 && ldk >= C * p * p && H >= p && W >= p);
   const int nh = H / p, nw = W / p;
   const long total = (long)B * nh * nw * ldk;
   const int grid = (int)min((total + 255) / 256, (long)8192);
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(1024) void image_rank_kernel(const int64_t* __restr
 }
 
 extern "C" int pg_image_rank(const int64_t* ids, int n, long image_id, int* rank, hipStream_t stream) {
-  PG_REQUIRE(n > 0);
+  PG_REQUIRE(ids && rank && n > 0);
   hipLaunchKernelGGL(image_rank_kernel, dim3(1), dim3(1024), 0, stream, ids, n, (int64_t)image_id, rank);
   PG_LAUNCH_CHECK();
   return 0;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void embed_merge_kernel(const int64_t* __restr
 extern "C" int pg_embed_merge(const int64_t* ids, const int* rank, int n, const void* embed, int V, const float* feat,
                               int n_feat, int H, long image_id, long pad_id, float img_scale, float normalizer,
                               float* out, hipStream_t stream) {
-  PG_REQUIRE(n > 0 && H % 4 == 0);
+  PG_REQUIRE(ids && embed && out && n > 0 && V > 0 && H > 0 && H % 4 == 0 && (n_feat == 0 || feat));
   hipLaunchKernelGGL(embed_merge_kernel, dim3(n), dim3(256), 0, stream, ids, rank, n, (const bf16_t*)embed, V, feat,
                      n_feat, H, (int64_t)image_id, (int64_t)pad_id, img_scale, normalizer, out);
   PG_LAUNCH_CHECK();
@@ -186,7 +186,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
 extern "C" int pg_rope_kv_write(void* qkv, int ldq, const int* pos, int T, int L, int Hq, int Hkv, int D,
                                 const float* cosT, const float* sinT, void* kc, void* vtc, int Smax, int slot_base,
                                 const int* slot_dev, hipStream_t stream) {
-  PG_REQUIRE(T > 0 && L > 0 && T % L == 0 && D % 2 == 0);
+  PG_REQUIRE(qkv && pos && cosT && sinT && kc && vtc && T > 0 && L > 0 && T % L == 0 && D % 2 == 0);
   hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, stream, (bf16_t*)qkv, ldq, pos, L, Hq, Hkv, D, cosT, sinT,
                      (bf16_t*)kc, (bf16_t*)vtc, Smax, slot_base, slot_dev);
   PG_LAUNCH_CHECK();
@@ -357,7 +357,8 @@ __global__ void argmax_merge_kernel(const float* __restrict__ pairs, int world, 
 
 extern "C" int pg_argmax_pairs(const float* logits, long ld, int B, int V, int vocab_offset, void* workspace,
                                float* pairs, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && V > 0 && ld % 4 == 0 && vocab_offset >= 0 && vocab_offset + V < (1 << 24));
+  PG_REQUIRE(logits && workspace && pairs && B > 0 && V > 0 && ld % 4 == 0 && vocab_offset >= 0 &&
+             vocab_offset + V < (1 << 24));
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
@@ -368,7 +369,7 @@ extern "C" int pg_argmax_pairs(const float* logits, long ld, int B, int V, int v
 
 extern "C" int pg_argmax_merge(const float* pairs, int world, int B, int64_t* out_ids, int64_t* hist, int hist_rows,
                                int* step, int* pos, int* kv_len, hipStream_t stream) {
-  PG_REQUIRE(world > 0 && B > 0 && (hist == nullptr || hist_rows > 0));
+  PG_REQUIRE(pairs && out_ids && world > 0 && B > 0 && (hist == nullptr || hist_rows > 0));
   hipLaunchKernelGGL(argmax_merge_kernel, dim3(1), dim3(64), 0, stream, pairs, world, B, out_ids, hist, hist_rows,
                      step, pos, kv_len);
   PG_LAUNCH_CHECK();
@@ -378,7 +379,7 @@ extern "C" int pg_argmax_merge(const float* pairs, int world, int B, int64_t* ou
 // workspace: >= B * AM_CHUNKS * 8 bytes
 extern "C" int pg_argmax(const float* logits, long ld, int B, int V, void* workspace, int64_t* out_ids,
                          int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && V > 0 && ld % 4 == 0 && (hist == nullptr || hist_rows > 0));
+  PG_REQUIRE(logits && workspace && out_ids && B > 0 && V > 0 && ld % 4 == 0 && (hist == nullptr || hist_rows > 0));
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
   hipLaunchKernelGGL(argmax_partial_kernel, dim3(AM_CHUNKS, B), dim3(256), 0, stream, logits, ld, V, pv, pi);
@@ -393,7 +394,8 @@ extern "C" int pg_argmax_embed(const float* logits, long ld, int B, int V, void*
                                int64_t* hist, int hist_rows, int* step, int* pos, int* kv_len, const void* embed,
                                int V_embed, const float* feat, int n_feat, int H, long image_id, long pad_id,
                                float img_scale, float normalizer, float* res, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && B <= AM_EMB_MAX_B && V > 0 && ld % 4 == 0 && (hist == nullptr || hist_rows > 0));
+  PG_REQUIRE(logits && workspace && out_ids && B > 0 && B <= AM_EMB_MAX_B && V > 0 && ld % 4 == 0 &&
+             (hist == nullptr || hist_rows > 0));
   PG_REQUIRE(embed != nullptr && res != nullptr && V_embed > 0 && H > 0 && H % 4 == 0 && (n_feat == 0 || feat));
   float* pv = (float*)workspace;
   int* pi = (int*)(pv + B * AM_CHUNKS);
@@ -540,7 +542,7 @@ __global__ void advance_kernel(int* step, int* kv_len) {
 extern "C" int pg_topp_sample(const float* logits, long ld, int B, int V, float temperature, float top_p,
                               const float* uniforms, int64_t* out_ids, int64_t* hist, int hist_rows, int* step, int* pos,
                               int* kv_len, float* probs_out, hipStream_t stream) {
-  PG_REQUIRE(B > 0 && V > 0 && temperature > 0.f && hist_rows > 0);
+  PG_REQUIRE(logits && uniforms && out_ids && B > 0 && V > 0 && temperature > 0.f && hist_rows > 0);
   hipLaunchKernelGGL(topp_kernel, dim3(B), dim3(1024), 0, stream, logits, ld, V, 1.0f / temperature, top_p, uniforms,
                      out_ids, hist, hist_rows, step, pos, B, kv_len, probs_out);
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, stream, step, kv_len);
@@ -573,7 +575,7 @@ __global__ void synth_kernel(void* out, long n, uint32_t seedmix, float a, float
 
 extern "C" int pg_synth_fill(void* out, long n, unsigned int seedmix, float a, float mean, int out_kind,
                              hipStream_t stream) {
-  PG_REQUIRE(n > 0 && n <= 0xFFFFFFFFl && (out_kind == 0 || out_kind == 1));
+  PG_REQUIRE(out && n > 0 && n <= 0xFFFFFFFFl && (out_kind == 0 || out_kind == 1));
   const int grid = (int)min((n + 255) / 256, (long)16384);
   hipLaunchKernelGGL(synth_kernel, dim3(grid), dim3(256), 0, stream, out, n, (uint32_t)seedmix, a, mean, out_kind);
   PG_LAUNCH_CHECK();
@@ -594,6 +596,7 @@ extern "C" int pg_abi_version(void) { return 13; }
 __attribute__((used)) static const char pg_source_hash_str[] = "PGHIP_SOURCE_HASH=" PG_SOURCE_HASH;
 extern "C" int pg_source_hash(char* out, int n) {
   const char* h = pg_source_hash_str + 18;
+  PG_REQUIRE(n <= 0 || out != nullptr);
   int i = 0;
   for (; h[i] && i + 1 < n; ++i) out[i] = h[i];
   if (n > 0) out[i] = 0;

@@ -182,7 +182,7 @@ static void norm_launch(int M_out, int H, int nsplit, hipStream_t stream, float*
 extern "C" int pg_norm_residual(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                                 const float* b, void* out, int ldo, float* out_f32, const int* row_map, int M_out,
                                 int H, int mode, float eps, int write_resid, hipStream_t stream) {
-  PG_REQUIRE(M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV);
+  PG_REQUIRE(resid && w && M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV);
   PG_REQUIRE(mode == 1 || b != nullptr);
   PG_REQUIRE(nsplit == 0 || partials != nullptr);
   norm_launch<false>(M_out, H, nsplit, stream, resid, partials, M_part, w, b, out, ldo, out_f32, row_map, mode, eps,
@@ -196,7 +196,7 @@ extern "C" int pg_norm_residual(float* resid, const float* partials, int nsplit,
 extern "C" int pg_norm_residual_fp8(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                                     const float* b, void* q, int ldq, float* scale, const int* row_map, int M_out,
                                     int H, int mode, float eps, int write_resid, hipStream_t stream) {
-  PG_REQUIRE(M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV && q != nullptr && scale != nullptr &&
+  PG_REQUIRE(resid && w && M_out > 0 && H > 0 && H % 4 == 0 && H <= 256 * 4 * NORM_MAXV && q != nullptr && scale != nullptr &&
              ldq >= H && ldq % 4 == 0);
   PG_REQUIRE(mode == 1 || b != nullptr);
   PG_REQUIRE(nsplit == 0 || partials != nullptr);
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(256) void norm_mx_kernel(float* __restrict__ resid,
 extern "C" int pg_norm_residual_mx(float* resid, const float* partials, int nsplit, int M_part, const float* w,
                                    void* q, int ldq, void* qs, float* ss, int ss_ld, int M, int H, int write_resid,
                                    hipStream_t stream) {
-  PG_REQUIRE(M > 0 && M <= M_part && H > 0 && H % 1024 == 0 && q && qs && ss && ldq >= H && ldq % 4 == 0 &&
+  PG_REQUIRE(resid && w && M > 0 && M <= M_part && H > 0 && H % 1024 == 0 && q && qs && ss && ldq >= H && ldq % 4 == 0 &&
              ss_ld >= H / 1024 && nsplit >= 0 && (nsplit == 0 || partials));
   PG_REQUIRE(((uintptr_t)resid & 15) == 0 && ((uintptr_t)w & 15) == 0 && ((uintptr_t)q & 3) == 0 &&
              ((uintptr_t)partials & 15) == 0);
